@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json headline: IQ Msamples/s (and x real-time) per GPU on the mode-0
+mono path, configs[1]: 101-tap RF LPF + 10x decimate + FM demod + 51-tap audio LPF / 5x
+decimate -> S16, on 1 GiB of synthetic 2.4 MS/s u8 I/Q resident in HBM.
+
+One "step" = one pass of the fused receive kernel over the whole 1 GiB stream (83,886 full
+reference blocks; the 1,024-byte tail is dropped like the reference drops partial blocks).
+Multi-GPU: one process per GPU (torch.distributed.run); every rank receives its own
+independent stream (weak scaling, no data-path collective); timing is the max over ranks.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+
+Prints ONE JSON line on rank 0.  `roofline` prices the fused kernel against HBM (SURVEY
+§8d algorithmic bytes: 2 B/IQ in + 2 B per mono audio frame out) from HIP-event kernel
+times on the context stream; `compute` gives the same kernel against the FP32 VALU roof.
+`cpu_baseline` times the reference's own src/filter.cpp mono path (oracle/_ref, 1 core) on
+the same bytes and reports whether its PCM equals the GPU's bit for bit.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+VALU_F32_PEAK_TOPS = 78.6      # 157.3 TF FP32 vector / 2: separate mul + add, no FMA
+RT_RATE = 2.4e6                # mode 0 real time: 2.4 MS/s complex
+STREAM_BYTES = 1 << 30         # BASELINE config 2: 1 GiB synthetic IQ
+RF_TAPS = 101
+
+
+def flops_per_iq(rf_taps: int) -> float:
+    # per IQ pair: RF 2 ch x taps x (mul+add) / 10, demod ~9/10, audio 51x2/50
+    return 2 * rf_taps * 2 / 10 + 0.9 + 51 * 2 / 50
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-bytes", type=int, default=STREAM_BYTES)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    import iqgen
+
+    fmrx = iqgen.load_fmrx()
+    rx = fmrx.Receiver(0, fmrx.MONO, rf_taps=RF_TAPS, device=local if world > 1 else 0)
+    bb, na = rx.geo.block_bytes, rx.geo.audio_frames
+    nb = STREAM_BYTES // bb
+    n_iq = nb * bb // 2
+    d_iq = torch.empty(STREAM_BYTES, dtype=torch.uint8, device="cuda")
+    d_pcm = torch.empty(nb * na, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    rx.synth_device(1000 + rank, 0, STREAM_BYTES // 2, d_iq.data_ptr())  # untimed input gen
+    rx.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        rx.process_device(d_iq.data_ptr(), nb, d_pcm.data_ptr())
+    rx.synchronize()
+    rx.kernel_timing(reset=1)  # arm per-launch HIP events on the context stream
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rx.process_device(d_iq.data_ptr(), nb, d_pcm.data_ptr())
+    rx.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms, launches = rx.kernel_timing(reset=-1)
+    if dist is not None:
+        t = torch.tensor([elapsed, kern_ms], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    total_iq = n_iq * args.steps * world
+    value = total_iq / elapsed / 1e6  # IQ Msamples/s, whole job
+    alg_bytes = 2 * n_iq + 2 * nb * na  # per launch: u8 I+Q in, S16 mono out
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    flops = flops_per_iq(RF_TAPS) * n_iq
+    line = {
+        "metric": "IQ Msamples/s (and x real-time) per GPU, mode-0 mono 2.4MS/s->48kS/s",
+        "value": round(value, 1),
+        "unit": "MS/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "x_realtime_per_gpu": round(value / world * 1e6 / RT_RATE, 1),
+        "config": {
+            "workload": "BASELINE configs[1]: mode-0 mono, 101-tap RF LPF + 10x decimate + FM demod "
+                        "+ 51-tap audio LPF/5x decimate -> S16, 1 GiB synthetic u8 IQ per GPU "
+                        "(83,886 reference blocks), device-resident",
+            "mode": 0, "channels": 1, "rf_taps": RF_TAPS, "stream_bytes_per_gpu": nb * bb,
+            "blocks_per_gpu": nb, "parallelism": f"streams x{world} (one independent stream per GPU)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "kernel": "mono_fused_kernel<101,10,5,256,3>",
+            "kernel_ms": round(kern_ms, 4),
+            "launches_timed": launches,
+            "alg_bytes_per_launch": alg_bytes,
+        },
+        "compute": {
+            "bound": "valu_f32_no_fma",
+            "achieved": round(flops / (kern_ms * 1e-3) / 1e12, 2),
+            "peak": VALU_F32_PEAK_TOPS,
+            "unit": "Tflop/s",
+            "frac": round(flops / (kern_ms * 1e-3) / 1e12 / VALU_F32_PEAK_TOPS, 4),
+            "flop_per_iq": round(flops_per_iq(RF_TAPS), 2),
+        },
+    }
+    traffic_file = os.path.join(REPO, "profiles", "traffic_mono101.json")
+    if os.path.exists(traffic_file):
+        with open(traffic_file) as f:
+            line["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
+
+    if rank == 0 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(d_iq, d_pcm, args.cpu_sample_bytes, bb, na)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(d_iq, d_pcm, sample_bytes, bb, na):
+    """The reference's own mono path (oracle/_ref: src/filter.cpp + src/iofunc.cpp, g++ -O3,
+    sequential project.cpp order, 1 core) on the first `sample_bytes` of the same stream."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    nbs = sample_bytes // bb
+    host = d_iq[: nbs * bb].cpu().numpy()
+    if oracle.reference_available():
+        ref, kind = oracle.Reference(), "reference"
+        t0 = time.perf_counter()
+        pcm = ref.run_mono(0, RF_TAPS, host)
+    else:
+        ref, kind = oracle.Oracle(), "port"
+        t0 = time.perf_counter()
+        pcm = ref.run(0, RF_TAPS, host, ["pcm_mono"])["pcm_mono"]
+    dt = time.perf_counter() - t0
+    # The GPU's last step re-processed the same 1 GiB with carried state, so compare the
+    # first sample from a fresh context.
+    import iqgen
+
+    fm = iqgen.load_fmrx()
+    fresh = fm.Receiver(0, fm.MONO, rf_taps=RF_TAPS)
+    out = d_pcm.new_empty(nbs * na)
+    fresh.process_device(d_iq.data_ptr(), nbs, out.data_ptr())
+    fresh.synchronize()
+    parity = bool(np.array_equal(out.cpu().numpy(), pcm))
+    fresh.close()
+    return {"value": round(nbs * bb / 2 / dt / 1e6, 2), "unit": "MS/s", "cores": 1, "kind": kind,
+            "sample": f"first {nbs} blocks ({nbs * bb} B, {nbs * bb / 2 / RT_RATE:.1f} s of signal) "
+                      f"of the rank-0 stream, sequential mono path",
+            "seconds": round(dt, 2), "bit_exact_vs_gpu": parity}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,135 @@
+/* include/fmrx.h — C ABI of the MI355X-native FM receive chain (libfmrx.so).
+ *
+ * Drop-in boundary for the per-block processing stage of the reference
+ * (mehtas30/Software-Defined-Radio-Course-Project).  Plain C types only: pointers, sizes,
+ * ints.  Every entry point returns an int status (FMRX_OK == 0, < 0 on error) instead of
+ * calling exit() like the reference does.
+ *
+ * Reference interfaces replaced (file:line under the reference tree):
+ *   fmrx_impulse_response_lpf  <- impulseResponseLPF   include/filter.h:15, src/filter.cpp:14-37
+ *   fmrx_impulse_response_bpf  <- impulseResponseBPF   include/filter.h:17, src/filter.cpp:39-64
+ *   fmrx_resample              <- resample             include/filter.h:19, src/filter.cpp:67-103
+ *   fmrx_fm_demod              <- FMDemod              include/filter.h:21, src/filter.cpp:106-133
+ *   fmrx_pll                   <- PLL                  include/filter.h:23, src/filter.cpp:136-174
+ *   fmrx_mixer                 <- mixer                include/filter.h:25, src/filter.cpp:176-184
+ *   fmrx_lr_extraction         <- LRExtraction         include/filter.h:27, src/filter.cpp:186-199
+ *   fmrx_normalize_iq          <- readStdinBlockData   include/iofunc.h:28, src/iofunc.cpp:62-69
+ *                                 + deinterleave       src/project.cpp:56-62
+ *   fmrx_rf_block              <- rf_thread loop body  src/project.cpp:48-70
+ *   fmrx_audio_block           <- audio_thread body    src/project.cpp:132-195
+ *   fmrx_process               <- both bodies fused (host buffers in, host PCM out)
+ *   fmrx_process_device        <- both bodies fused, device-resident buffers, async
+ *
+ * Buffers: functions named *_device / fmrx_resample etc. take DEVICE pointers and enqueue on
+ * the context's HIP stream; fmrx_rf_block / fmrx_audio_block / fmrx_process take HOST
+ * pointers and return when the result is in host memory.  The caller owns every buffer.
+ */
+#ifndef FMRX_H
+#define FMRX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FMRX_OK 0
+#define FMRX_EINVAL (-1)   /* bad argument / configuration */
+#define FMRX_EHIP (-2)     /* HIP runtime error (no device, launch failure, ...) */
+#define FMRX_ENOMEM (-3)   /* device or host allocation failed */
+#define FMRX_ESTATE (-4)   /* state blob size/version mismatch */
+
+/* Output semantics (SURVEY §7 hard part 3). */
+#define FMRX_STEREO 2        /* project.cpp output: S16 interleaved R,L; shared audio_state  */
+#define FMRX_MONO 1          /* mono S16 with a private audio history (project.cpp:146 with  */
+                             /* its own state vector: fmMonoBlock-style receiver)            */
+
+typedef struct {
+    int mode;        /* 0..3, src/project.cpp:327-362                                         */
+    int channels;    /* FMRX_MONO or FMRX_STEREO                                              */
+    int rf_taps;     /* RF LPF taps, reference 51 (project.cpp:306); 0 = default              */
+    int bp_taps;     /* stereo band-pass taps, reference 51 (project.cpp:307); 0 = default   */
+    int audio_taps;  /* audio LPF taps per phase, reference 51 (project.cpp:319; x up in 2/3) */
+    int n_streams;   /* independent IQ streams processed per call (>=1)                        */
+    int device;      /* HIP device ordinal                                                     */
+} fmrx_config;
+
+typedef struct {
+    int rf_fs, rf_decim, if_fs, bp_fs, audio_up, audio_down;
+    int rf_taps, bp_taps, audio_taps_total; /* audio_taps_total = audio_taps * audio_up      */
+    size_t block_bytes;   /* u8 per block, project.cpp:364 (256 * rf_decim * audio_decim)     */
+    size_t iq_pairs;      /* block_bytes / 2                                                  */
+    size_t if_samples;    /* demod floats per block                                           */
+    size_t audio_frames;  /* audio frames per block                                           */
+    size_t pcm_samples;   /* int16 per block = audio_frames * channels                        */
+} fmrx_geometry_t;
+
+typedef struct fmrx_ctx fmrx_ctx;
+
+/* ---- configuration & lifetime ------------------------------------------------------- */
+int fmrx_config_default(fmrx_config* cfg, int mode, int channels);
+int fmrx_geometry(const fmrx_config* cfg, fmrx_geometry_t* geo);
+int fmrx_create(const fmrx_config* cfg, fmrx_ctx** out);
+void fmrx_destroy(fmrx_ctx* ctx);
+int fmrx_reset(fmrx_ctx* ctx);                         /* back to the power-on state        */
+const char* fmrx_last_error(void);                     /* thread-local message              */
+const char* fmrx_version(void);
+
+/* ---- stream state (checkpoint / resume) ---------------------------------------------- */
+int fmrx_state_size(const fmrx_ctx* ctx, size_t* bytes);
+int fmrx_get_state(fmrx_ctx* ctx, void* buf, size_t bytes);
+int fmrx_set_state(fmrx_ctx* ctx, const void* buf, size_t bytes);
+
+/* ---- block-streaming entry points (host buffers; stream-major for n_streams > 1) ------ */
+/* iq: n_streams x (n_blocks * block_bytes) u8; pcm: n_streams x (n_blocks * pcm_samples).  */
+int fmrx_process(fmrx_ctx* ctx, const uint8_t* iq, size_t n_blocks, int16_t* pcm);
+/* Split stages, the reference's thread split (project.cpp:19-85 | 87-197).
+ * demod: n_streams x (n_blocks * if_samples) float.                                        */
+int fmrx_rf_block(fmrx_ctx* ctx, const uint8_t* iq, size_t n_blocks, float* demod);
+int fmrx_audio_block(fmrx_ctx* ctx, const float* demod, size_t n_blocks, int16_t* pcm);
+
+/* ---- device-resident fused path (async on the context stream) ------------------------ */
+int fmrx_process_device(fmrx_ctx* ctx, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm);
+/* Optional float taps of the mono product (n_streams x n_blocks*audio_frames), may be NULL */
+int fmrx_process_device_ex(fmrx_ctx* ctx, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
+                           float* d_mono);
+int fmrx_synchronize(fmrx_ctx* ctx);
+void* fmrx_stream(fmrx_ctx* ctx);                       /* the hipStream_t used               */
+/* Device time of the fused RF/demod/audio kernel, from HIP event pairs recorded around each
+ * launch on the context stream (no host sync in between).  Returns the average over the
+ * launches recorded since the last reset.  reset > 0: clear and arm recording; reset < 0:
+ * clear and disarm; 0: just read.                                                         */
+int fmrx_kernel_timing(fmrx_ctx* ctx, int reset, double* avg_ms, long* launches);
+
+/* ---- filter.h primitives on device buffers (context stream; s = per-call state) ------- */
+int fmrx_impulse_response_lpf(float* h, float fs, float fc, int taps, int gain);      /* host */
+int fmrx_impulse_response_bpf(float* h, float fs, float fb, float fe, int taps);      /* host */
+/* d_state: taps-1 floats (in/out).  Returns the output count in *n_out.                    */
+int fmrx_resample(fmrx_ctx* ctx, float* d_out, float* d_state, const float* d_in, int n_in,
+                  const float* d_coeff, int taps, int up, int down, int* n_out);
+/* d_prev: 2 floats {prev_i, prev_q} (in/out).                                              */
+int fmrx_fm_demod(fmrx_ctx* ctx, float* d_out, float* d_prev, const float* d_i,
+                  const float* d_q, int n);
+/* d_io: PLL input, overwritten by the NCO output.  d_st: 6 floats {integrator, phaseEst,
+ * feedbackI, feedbackQ, ncoOut_state, trigOffset} (in/out).                                */
+int fmrx_pll(fmrx_ctx* ctx, float* d_io, int n, float freq, float fs, float nco_scale,
+             float phase_adjust, float norm_bw, float* d_st);
+int fmrx_mixer(fmrx_ctx* ctx, float* d_out, const float* d_a, const float* d_b, int n);
+int fmrx_lr_extraction(fmrx_ctx* ctx, float* d_left, float* d_right, const float* d_mono,
+                       const float* d_stereo, int n);
+/* u8 interleaved I,Q -> float I and Q (n_pairs each), iofunc.cpp:67 normalisation.        */
+int fmrx_normalize_iq(fmrx_ctx* ctx, const uint8_t* d_iq, size_t n_pairs, float* d_i, float* d_q);
+/* S16 quantiser of project.cpp:185-191 (NaN -> 0, x86 truncation + 16-bit wrap).           */
+int fmrx_quantize(fmrx_ctx* ctx, const float* d_x, size_t n, int16_t* d_out);
+
+/* ---- deterministic synthetic FM-stereo IQ; identical bytes host/device ---- */
+/* Stream `seed`, samples [first_pair, first_pair+n_pairs) of a stream at rf_fs.            */
+int fmrx_synth_host(uint64_t seed, int rf_fs, uint64_t first_pair, size_t n_pairs, uint8_t* out);
+int fmrx_synth_device(fmrx_ctx* ctx, uint64_t seed, int rf_fs, uint64_t first_pair,
+                      size_t n_pairs, uint8_t* d_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FMRX_H */

@@ -1,0 +1,699 @@
+// api.cpp — the C ABI of include/fmrx.h: context lifetime, per-stream state, the block-
+// streaming entry points and the filter.h primitive mirror.  Host C++ driving the HIP
+// kernels of mono_fused.hip / stereo.hip / prims.hip on one device and one HIP stream per
+// context.  No CPU compute path exists: every numeric result comes from a GPU kernel.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/fmrx.h"
+#include "fmrx_internal.h"
+#include "synth.h"
+
+using namespace fmrx;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return fail(FMRX_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),     \
+                        __FILE__, __LINE__);                                           \
+    } while (0)
+
+constexpr int kDemodHist = 64;   // demod samples kept in front of each call (>= bp_taps-1)
+constexpr int kMixTail = 64;     // must match stereo.hip kTail
+constexpr uint32_t kStateMagic = 0x46524D58u;  // "FMRX"
+constexpr uint32_t kStateVersion = 1;
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    int ensure(size_t count) {
+        if (count <= n) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T)) != hipSuccess) {
+            p = nullptr;
+            return fail(FMRX_ENOMEM, "hipMalloc of %zu bytes failed", count * sizeof(T));
+        }
+        n = count;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+}  // namespace
+
+struct fmrx_ctx {
+    fmrx_config cfg{};
+    fmrx_geometry_t geo{};
+    ModeConstants mc{};
+    hipStream_t stream = nullptr;
+    // taps (host) and device copies
+    std::vector<float> rf, audio, ch, ca;
+    MonoTaps mono_taps{};
+    DevBuf<float> d_audio, d_rf;
+    // RF state: the raw bytes preceding the next call, double-buffered
+    size_t halo_bytes = 0;
+    DevBuf<uint8_t> d_halo[2];
+    int halo_cur = 0;
+    // audio state of the mono product: last (audio_taps_total - 1) demod samples
+    int audio_hist = 0;
+    DevBuf<float> d_audio_hist;
+    // stereo engine state
+    DevBuf<float> d_demod;        // n_streams x (kDemodHist + cap_if)
+    size_t demod_stride = 0;
+    DevBuf<float> d_channel, d_carrier;
+    DevBuf<float> d_pll;          // n_streams x 8
+    DevBuf<float> d_mix_tail;     // n_streams x kMixTail
+    DevBuf<float> d_mono_state;   // n_streams x 8
+    // staging for the host-buffer entry points
+    DevBuf<uint8_t> d_in;
+    DevBuf<int16_t> d_out;
+    DevBuf<float> d_f32;
+    DevBuf<float> d_scratch;
+    DevBuf<int16_t> d_sintab;
+    // kernel timing: pairs of HIP events recorded around each fused-kernel launch on the
+    // context stream (no host sync inside the timed loop); read by fmrx_kernel_timing
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
+    size_t ev_used = 0;
+    bool timing = false;
+};
+
+namespace {
+
+bool fused_rf_supported(const fmrx_ctx* c) {
+    const int t = c->geo.rf_taps, d = c->geo.rf_decim;
+    return (t == 51 || t == 101) && (d == 10 || d == 4);
+}
+
+int set_device(const fmrx_ctx* c) {
+    HIPCHK(hipSetDevice(c->cfg.device));
+    return 0;
+}
+
+int reset_state(fmrx_ctx* c) {
+    const int ns = c->cfg.n_streams;
+    HIPCHK(hipMemsetAsync(c->d_halo[0].p, 0x80, c->halo_bytes * ns, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_halo[1].p, 0x80, c->halo_bytes * ns, c->stream));
+    c->halo_cur = 0;
+    HIPCHK(hipMemsetAsync(c->d_audio_hist.p, 0, sizeof(float) * c->audio_hist * ns, c->stream));
+    if (c->d_demod.p)
+        HIPCHK(hipMemsetAsync(c->d_demod.p, 0, sizeof(float) * c->d_demod.n, c->stream));
+    // project.cpp:106-111: integrator 0, phaseEst 0, feedbackI 1, feedbackQ 0,
+    // ncoOut_state 1, trigOffset 0
+    std::vector<float> pll(8 * ns, 0.0f);
+    for (int s = 0; s < ns; s++) {
+        pll[8 * s + 2] = 1.0f;
+        pll[8 * s + 4] = 1.0f;
+    }
+    HIPCHK(hipMemcpyAsync(c->d_pll.p, pll.data(), sizeof(float) * pll.size(),
+                          hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_mix_tail.p, 0, sizeof(float) * kMixTail * ns, c->stream));
+    HIPCHK(hipMemsetAsync(c->d_mono_state.p, 0, sizeof(float) * 8 * ns, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// Segments per stream for the fused kernel: enough workgroups to fill the chip
+// (2 resident per CU on 256 CUs) without making segments so short that the pre-roll chunk
+// dominates.
+int mono_segments(const fmrx_ctx* c, long long n_if) {
+    const long long chunks = mono_chunks(n_if, c->geo.rf_taps, c->geo.rf_decim, c->geo.audio_down);
+    const long long target_wg = 512;
+    long long segs = std::max<long long>(1, target_wg / std::max(1, c->cfg.n_streams));
+    segs = std::min(segs, std::max<long long>(1, chunks / 4));
+    return (int)std::max<long long>(1, segs);
+}
+
+// RF front end (+ the mono audio stage when `pcm` is non-null and the mode allows it).
+int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm, float* d_mono,
+              float* d_demod, size_t demod_stride, int demod_hist, bool with_audio) {
+    const int ns = c->cfg.n_streams;
+    MonoLaunch L{};
+    L.iq = d_iq;
+    L.halo = c->d_halo[c->halo_cur].p;
+    L.pcm = d_pcm;
+    L.mono = d_mono;
+    L.demod = d_demod;
+    L.demod_stride = demod_stride;
+    L.demod_hist = demod_hist;
+    // the mono product's audio history stays in step with the stream (split-API use)
+    L.demod_tail = (c->geo.audio_up == 1) ? c->d_audio_hist.p : nullptr;
+    L.stream_bytes = n_blocks * c->geo.block_bytes;
+    L.halo_bytes = c->halo_bytes;
+    L.n_if = (long long)(n_blocks * c->geo.if_samples);
+    L.segs = mono_segments(c, L.n_if);
+    L.audio = with_audio ? 1 : 0;
+    const int ad = c->geo.audio_up == 1 ? c->geo.audio_down : 5;
+    std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
+    if (c->timing) {
+        if (c->ev_used == c->evs.size()) {
+            std::pair<hipEvent_t, hipEvent_t> e{nullptr, nullptr};
+            HIPCHK(hipEventCreate(&e.first));
+            HIPCHK(hipEventCreate(&e.second));
+            c->evs.push_back(e);
+        }
+        ev = &c->evs[c->ev_used++];
+        HIPCHK(hipEventRecord(ev->first, c->stream));
+    }
+    int rc = launch_mono_fused(L, ns, c->geo.rf_taps, c->geo.rf_decim, ad, c->mono_taps, c->stream);
+    if (rc != 0) return fail(rc == -1 ? FMRX_EINVAL : FMRX_EHIP, "fused kernel launch failed (%d)", rc);
+    if (ev) HIPCHK(hipEventRecord(ev->second, c->stream));
+    rc = launch_halo_update(d_iq, L.stream_bytes, c->d_halo[c->halo_cur].p,
+                            c->d_halo[c->halo_cur ^ 1].p, c->halo_bytes, ns, c->stream);
+    if (rc != 0) return fail(FMRX_EHIP, "halo update failed");
+    c->halo_cur ^= 1;
+    return 0;
+}
+
+// Mono product audio stage on a demod buffer (generic polyphase path: modes 2/3 and the
+// split API).  demod: ns x n_if contiguous.  Advances d_audio_hist.
+int run_mono_audio(fmrx_ctx* c, const float* d_demod, size_t demod_stride, size_t n_if,
+                   int16_t* d_pcm, float* d_mono) {
+    const int ns = c->cfg.n_streams;
+    const int at = c->geo.audio_taps_total;
+    const size_t na = n_if * c->geo.audio_up / c->geo.audio_down;
+    int rc = c->d_scratch.ensure(na * ns);
+    if (rc) return rc;
+    for (int s = 0; s < ns; s++) {
+        const float* in = d_demod + s * demod_stride;
+        float* st = c->d_audio_hist.p + (size_t)s * c->audio_hist;
+        float* out = d_mono ? d_mono + s * na : c->d_scratch.p + s * na;
+        rc = launch_resample(out, st, in, (int)n_if, c->d_audio.p, at, c->geo.audio_up,
+                             c->geo.audio_down, (int)na, c->stream);
+        if (rc == 0) rc = launch_tail_copy(st, in + (n_if - (at - 1)), at - 1, c->stream);
+        if (rc == 0) rc = launch_quantize(out, na, d_pcm + s * na, c->stream);
+        if (rc) return fail(FMRX_EHIP, "mono audio stage launch failed");
+    }
+    return 0;
+}
+
+// Stereo engine on c->d_demod (history in front, n_if new samples per stream).
+int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono) {
+    const int ns = c->cfg.n_streams;
+    const size_t n_if = n_blocks * c->geo.if_samples;
+    int rc = c->d_channel.ensure(n_if * ns);
+    if (!rc) rc = c->d_carrier.ensure(n_if * ns);
+    if (rc) return rc;
+    StereoLaunch S{};
+    S.demod = c->d_demod.p;
+    S.channel = c->d_channel.p;
+    S.carrier = c->d_carrier.p;
+    S.n_if = (int)n_if;
+    S.hist = kDemodHist;
+    S.demod_stride = c->demod_stride;
+    S.ch_c = c->ch.data();
+    S.ca_c = c->ca.data();
+    S.bp_taps = c->geo.bp_taps;
+    if (launch_bpf_pair(S, ns, c->stream)) return fail(FMRX_EHIP, "band-pass launch failed");
+    // project.cpp:166: PLL(carrier, 19000, if_fs, 2, 0, 0.01, ...)
+    if (launch_pll(c->d_carrier.p, (int)n_if, ns, n_if, 19000.0f, (float)c->geo.if_fs, 2.0f, 0.0f,
+                   0.01f, c->d_pll.p, c->stream))
+        return fail(FMRX_EHIP, "PLL launch failed");
+    AudioLaunch A{};
+    A.demod = c->d_demod.p;
+    A.demod_stride = c->demod_stride;
+    A.hist = kDemodHist;
+    A.channel = c->d_channel.p;
+    A.nco = c->d_carrier.p;
+    A.mix_tail = c->d_mix_tail.p;
+    A.mono_state = c->d_mono_state.p;
+    A.pcm = d_pcm;
+    A.mono_out = d_mono;
+    A.n_blocks = (int)n_blocks;
+    A.if_per_block = (int)c->geo.if_samples;
+    A.frames_per_block = (int)c->geo.audio_frames;
+    A.up = c->geo.audio_up;
+    A.down = c->geo.audio_down;
+    A.at = c->geo.audio_taps_total;
+    A.audio_c = c->d_audio.p;
+    if (launch_stereo_audio(A, ns, c->stream)) return fail(FMRX_EHIP, "stereo audio launch failed");
+    // demod history for the next call: last kDemodHist samples -> front
+    for (int s = 0; s < ns; s++) {
+        float* base = c->d_demod.p + (size_t)s * c->demod_stride;
+        if (launch_tail_copy(base, base + n_if, kDemodHist, c->stream))
+            return fail(FMRX_EHIP, "demod history copy failed");
+    }
+    return 0;
+}
+
+int ensure_demod(fmrx_ctx* c, size_t n_if) {
+    const size_t stride = kDemodHist + n_if;
+    if (stride <= c->demod_stride) return 0;
+    // grow, preserving the history of every stream
+    DevBuf<float> nb;
+    int rc = nb.ensure(stride * c->cfg.n_streams);
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(nb.p, 0, sizeof(float) * nb.n, c->stream));
+    if (c->d_demod.p) {
+        HIPCHK(hipMemcpy2DAsync(nb.p, stride * sizeof(float), c->d_demod.p,
+                                c->demod_stride * sizeof(float), kDemodHist * sizeof(float),
+                                c->cfg.n_streams, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c->d_demod.release();
+    }
+    c->d_demod = nb;
+    c->demod_stride = stride;
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fmrx_last_error(void) { return g_err.c_str(); }
+const char* fmrx_version(void) { return "fmrx 0.1 (gfx950)"; }
+
+int fmrx_config_default(fmrx_config* cfg, int mode, int channels) {
+    if (!cfg) return fail(FMRX_EINVAL, "null config");
+    ModeConstants m;
+    if (!mode_constants(mode, &m)) return fail(FMRX_EINVAL, "invalid mode %d", mode);
+    if (channels != FMRX_MONO && channels != FMRX_STEREO)
+        return fail(FMRX_EINVAL, "invalid channels %d", channels);
+    cfg->mode = mode;
+    cfg->channels = channels;
+    cfg->rf_taps = 51;     // src/project.cpp:306
+    cfg->bp_taps = 51;     // src/project.cpp:307
+    cfg->audio_taps = 51;  // src/project.cpp:319
+    cfg->n_streams = 1;
+    cfg->device = 0;
+    return FMRX_OK;
+}
+
+int fmrx_geometry(const fmrx_config* cfg, fmrx_geometry_t* g) {
+    if (!cfg || !g) return fail(FMRX_EINVAL, "null argument");
+    ModeConstants m;
+    if (!mode_constants(cfg->mode, &m)) return fail(FMRX_EINVAL, "invalid mode %d", cfg->mode);
+    if (cfg->channels != FMRX_MONO && cfg->channels != FMRX_STEREO)
+        return fail(FMRX_EINVAL, "invalid channels %d", cfg->channels);
+    const int rf_taps = cfg->rf_taps ? cfg->rf_taps : 51;
+    const int bp_taps = cfg->bp_taps ? cfg->bp_taps : 51;
+    const int audio_taps = cfg->audio_taps ? cfg->audio_taps : 51;
+    if (rf_taps < 3 || rf_taps > kMaxRfTaps) return fail(FMRX_EINVAL, "rf_taps %d out of range", rf_taps);
+    if (bp_taps < 3 || bp_taps > 64) return fail(FMRX_EINVAL, "bp_taps %d out of range", bp_taps);
+    if (audio_taps < 3 || audio_taps > kMaxAudioTaps)
+        return fail(FMRX_EINVAL, "audio_taps %d out of range", audio_taps);
+    g->rf_fs = m.rf_fs;
+    g->rf_decim = m.rf_decim;
+    g->if_fs = m.if_fs;
+    g->bp_fs = m.bp_fs;
+    g->audio_up = m.audio_up;
+    g->audio_down = m.audio_down;
+    g->rf_taps = rf_taps;
+    g->bp_taps = bp_taps;
+    g->audio_taps_total = audio_taps * m.audio_up;  // project.cpp:347,356
+    g->block_bytes = (size_t)256 * m.rf_decim * m.audio_down;  // project.cpp:364
+    g->iq_pairs = g->block_bytes / 2;
+    g->if_samples = g->iq_pairs / m.rf_decim;
+    g->audio_frames = g->if_samples * m.audio_up / m.audio_down;
+    g->pcm_samples = g->audio_frames * cfg->channels;
+    if ((size_t)g->audio_taps_total - 1 > g->if_samples || (size_t)rf_taps - 1 > g->iq_pairs)
+        return fail(FMRX_EINVAL, "filter longer than a block");
+    return FMRX_OK;
+}
+
+int fmrx_create(const fmrx_config* cfg, fmrx_ctx** out) {
+    if (!out) return fail(FMRX_EINVAL, "null output pointer");
+    *out = nullptr;
+    fmrx_geometry_t g;
+    int rc = fmrx_geometry(cfg, &g);
+    if (rc) return rc;
+    if (cfg->n_streams < 1) return fail(FMRX_EINVAL, "n_streams must be >= 1");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(FMRX_EHIP, "no HIP device available (libfmrx has no CPU path)");
+    if (cfg->device < 0 || cfg->device >= ndev) return fail(FMRX_EINVAL, "bad device %d", cfg->device);
+    fmrx_ctx* c = new fmrx_ctx();
+    c->cfg = *cfg;
+    c->cfg.rf_taps = g.rf_taps;
+    c->cfg.bp_taps = g.bp_taps;
+    c->geo = g;
+    mode_constants(cfg->mode, &c->mc);
+    if (!fused_rf_supported(c)) {
+        delete c;
+        return fail(FMRX_EINVAL, "no compiled RF kernel for rf_taps=%d rf_decim=%d", g.rf_taps,
+                    g.rf_decim);
+    }
+    if ((rc = set_device(c))) { delete c; return rc; }
+    // taps, exactly as the reference designs them (project.cpp:37, 97, 104, 117)
+    c->rf.resize(g.rf_taps);
+    design_lpf(c->rf.data(), (float)g.rf_fs, (float)kRfFc, g.rf_taps, 1);
+    c->audio.resize(g.audio_taps_total);
+    design_lpf(c->audio.data(), (float)g.if_fs, (float)kAudioFc, g.audio_taps_total, g.audio_up);
+    c->ch.resize(g.bp_taps);
+    design_bpf(c->ch.data(), (float)g.bp_fs, 22000.0f, 54000.0f, g.bp_taps);
+    c->ca.resize(g.bp_taps);
+    design_bpf(c->ca.data(), (float)g.bp_fs, 18500.0f, 19500.0f, g.bp_taps);
+    std::memset(&c->mono_taps, 0, sizeof c->mono_taps);
+    std::copy(c->rf.begin(), c->rf.end(), c->mono_taps.rf);
+    if (g.audio_up == 1) std::copy(c->audio.begin(), c->audio.end(), c->mono_taps.audio);
+
+    const int ns = cfg->n_streams;
+    auto cleanup = [&](int code) { fmrx_destroy(c); return code; };
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+        return cleanup(fail(FMRX_EHIP, "hipStreamCreate failed"));
+    c->halo_bytes = mono_halo_bytes(g.rf_taps, g.rf_decim, g.audio_down);
+    c->audio_hist = g.audio_taps_total - 1;
+    if ((rc = c->d_halo[0].ensure(c->halo_bytes * ns)) || (rc = c->d_halo[1].ensure(c->halo_bytes * ns)) ||
+        (rc = c->d_audio_hist.ensure((size_t)c->audio_hist * ns)) ||
+        (rc = c->d_audio.ensure(c->audio.size())) || (rc = c->d_rf.ensure(c->rf.size())) ||
+        (rc = c->d_pll.ensure(8 * (size_t)ns)) || (rc = c->d_mix_tail.ensure((size_t)kMixTail * ns)) ||
+        (rc = c->d_mono_state.ensure(8 * (size_t)ns)) || (rc = c->d_sintab.ensure(kSinSize)))
+        return cleanup(rc);
+    if (hipMemcpy(c->d_audio.p, c->audio.data(), sizeof(float) * c->audio.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_rf.p, c->rf.data(), sizeof(float) * c->rf.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->d_sintab.p, synth_sintab(), sizeof(int16_t) * kSinSize, hipMemcpyHostToDevice) != hipSuccess)
+        return cleanup(fail(FMRX_EHIP, "tap upload failed"));
+    if ((rc = reset_state(c))) return cleanup(rc);
+    *out = c;
+    return FMRX_OK;
+}
+
+void fmrx_destroy(fmrx_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->cfg.device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    c->d_audio.release(); c->d_rf.release(); c->d_halo[0].release(); c->d_halo[1].release();
+    c->d_audio_hist.release(); c->d_demod.release(); c->d_channel.release(); c->d_carrier.release();
+    c->d_pll.release(); c->d_mix_tail.release(); c->d_mono_state.release(); c->d_in.release();
+    c->d_out.release(); c->d_f32.release(); c->d_scratch.release(); c->d_sintab.release();
+    for (auto& e : c->evs) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int fmrx_reset(fmrx_ctx* c) {
+    if (!c) return fail(FMRX_EINVAL, "null context");
+    int rc = set_device(c);
+    return rc ? rc : reset_state(c);
+}
+
+// ---- state blob: header + halo bytes + audio history + stereo state ------------------
+int fmrx_state_size(const fmrx_ctx* c, size_t* bytes) {
+    if (!c || !bytes) return fail(FMRX_EINVAL, "null argument");
+    const size_t ns = c->cfg.n_streams;
+    *bytes = 8 * sizeof(uint32_t) + ns * (c->halo_bytes + sizeof(float) * (c->audio_hist + kDemodHist + 8 + kMixTail + 8));
+    return FMRX_OK;
+}
+
+namespace {
+struct BlobIO {
+    uint8_t* p;
+    bool put;
+    int io(fmrx_ctx* c, void* dev, size_t n) {
+        if (n == 0) return 0;
+        if (put) HIPCHK(hipMemcpyAsync(dev, p, n, hipMemcpyHostToDevice, c->stream));
+        else HIPCHK(hipMemcpyAsync(p, dev, n, hipMemcpyDeviceToHost, c->stream));
+        p += n;
+        return 0;
+    }
+};
+
+int state_io(fmrx_ctx* c, uint8_t* buf, size_t bytes, bool put) {
+    size_t need;
+    fmrx_state_size(c, &need);
+    if (bytes < need) return fail(FMRX_ESTATE, "state buffer too small (%zu < %zu)", bytes, need);
+    int rc = set_device(c);
+    if (rc) return rc;
+    uint32_t hdr[8] = {kStateMagic, kStateVersion, (uint32_t)c->cfg.mode, (uint32_t)c->cfg.channels,
+                       (uint32_t)c->geo.rf_taps, (uint32_t)c->cfg.n_streams, (uint32_t)c->halo_bytes,
+                       (uint32_t)c->audio_hist};
+    if (put) {
+        if (std::memcmp(hdr, buf, sizeof hdr) != 0) return fail(FMRX_ESTATE, "state blob does not match this context");
+    } else {
+        std::memcpy(buf, hdr, sizeof hdr);
+    }
+    const size_t ns = c->cfg.n_streams;
+    if (put && (rc = ensure_demod(c, 1))) return rc;
+    if (!put && !c->d_demod.p && (rc = ensure_demod(c, 1))) return rc;
+    BlobIO b{buf + sizeof hdr, put};
+    if ((rc = b.io(c, c->d_halo[c->halo_cur].p, ns * c->halo_bytes))) return rc;
+    if ((rc = b.io(c, c->d_audio_hist.p, ns * sizeof(float) * c->audio_hist))) return rc;
+    for (size_t s = 0; s < ns; s++)
+        if ((rc = b.io(c, c->d_demod.p + s * c->demod_stride, sizeof(float) * kDemodHist))) return rc;
+    if ((rc = b.io(c, c->d_pll.p, ns * sizeof(float) * 8))) return rc;
+    if ((rc = b.io(c, c->d_mix_tail.p, ns * sizeof(float) * kMixTail))) return rc;
+    if ((rc = b.io(c, c->d_mono_state.p, ns * sizeof(float) * 8))) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+}  // namespace
+
+int fmrx_get_state(fmrx_ctx* c, void* buf, size_t bytes) {
+    if (!c || !buf) return fail(FMRX_EINVAL, "null argument");
+    return state_io(c, static_cast<uint8_t*>(buf), bytes, false);
+}
+
+int fmrx_set_state(fmrx_ctx* c, const void* buf, size_t bytes) {
+    if (!c || !buf) return fail(FMRX_EINVAL, "null argument");
+    return state_io(c, static_cast<uint8_t*>(const_cast<void*>(buf)), bytes, true);
+}
+
+// ---- fused device-resident path ----------------------------------------------------------
+int fmrx_process_device_ex(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
+                           float* d_mono) {
+    if (!c || !d_iq || !d_pcm) return fail(FMRX_EINVAL, "null argument");
+    if (n_blocks == 0) return FMRX_OK;
+    int rc = set_device(c);
+    if (rc) return rc;
+    const size_t n_if = n_blocks * c->geo.if_samples;
+    if (c->cfg.channels == FMRX_MONO && c->geo.audio_up == 1)
+        return run_fused(c, d_iq, n_blocks, d_pcm, d_mono, nullptr, 0, 0, true);
+    if (c->cfg.channels == FMRX_MONO) {
+        // modes 2/3: fused RF -> demod buffer, then the polyphase audio stage
+        if ((rc = c->d_f32.ensure(n_if * c->cfg.n_streams))) return rc;
+        if ((rc = run_fused(c, d_iq, n_blocks, nullptr, nullptr, c->d_f32.p, n_if, 0, false))) return rc;
+        return run_mono_audio(c, c->d_f32.p, n_if, n_if, d_pcm, d_mono);
+    }
+    if ((rc = ensure_demod(c, n_if))) return rc;
+    if ((rc = run_fused(c, d_iq, n_blocks, nullptr, nullptr, c->d_demod.p, c->demod_stride,
+                        kDemodHist, false)))
+        return rc;
+    return run_stereo_audio(c, n_blocks, d_pcm, d_mono);
+}
+
+int fmrx_process_device(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm) {
+    return fmrx_process_device_ex(c, d_iq, n_blocks, d_pcm, nullptr);
+}
+
+int fmrx_synchronize(fmrx_ctx* c) {
+    if (!c) return fail(FMRX_EINVAL, "null context");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return FMRX_OK;
+}
+
+void* fmrx_stream(fmrx_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int fmrx_kernel_timing(fmrx_ctx* c, int reset, double* avg_ms, long* launches) {
+    if (!c) return fail(FMRX_EINVAL, "null context");
+    int rc = set_device(c);
+    if (rc) return rc;
+    double total = 0.0;
+    if (c->ev_used) HIPCHK(hipEventSynchronize(c->evs[c->ev_used - 1].second));
+    for (size_t i = 0; i < c->ev_used; i++) {
+        float ms = 0.0f;
+        HIPCHK(hipEventElapsedTime(&ms, c->evs[i].first, c->evs[i].second));
+        total += ms;
+    }
+    if (avg_ms) *avg_ms = c->ev_used ? total / (double)c->ev_used : 0.0;
+    if (launches) *launches = (long)c->ev_used;
+    if (reset > 0) {  // reset > 0: clear and arm event timing of the fused kernel
+        c->ev_used = 0;
+        c->timing = true;
+    } else if (reset < 0) {  // reset < 0: clear and disarm
+        c->ev_used = 0;
+        c->timing = false;
+    }
+    return FMRX_OK;
+}
+
+// ---- host-buffer entry points ---------------------------------------------------------------
+int fmrx_process(fmrx_ctx* c, const uint8_t* iq, size_t n_blocks, int16_t* pcm) {
+    if (!c || !iq || !pcm) return fail(FMRX_EINVAL, "null argument");
+    if (n_blocks == 0) return FMRX_OK;
+    int rc = set_device(c);
+    if (rc) return rc;
+    const size_t ns = c->cfg.n_streams;
+    const size_t in_bytes = ns * n_blocks * c->geo.block_bytes;
+    const size_t out_n = ns * n_blocks * c->geo.pcm_samples;
+    if ((rc = c->d_in.ensure(in_bytes)) || (rc = c->d_out.ensure(out_n))) return rc;
+    HIPCHK(hipMemcpyAsync(c->d_in.p, iq, in_bytes, hipMemcpyHostToDevice, c->stream));
+    if ((rc = fmrx_process_device(c, c->d_in.p, n_blocks, c->d_out.p))) return rc;
+    HIPCHK(hipMemcpyAsync(pcm, c->d_out.p, out_n * sizeof(int16_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return FMRX_OK;
+}
+
+// rf_thread body (project.cpp:48-70): u8 blocks -> demod floats.
+int fmrx_rf_block(fmrx_ctx* c, const uint8_t* iq, size_t n_blocks, float* demod) {
+    if (!c || !iq || !demod) return fail(FMRX_EINVAL, "null argument");
+    if (n_blocks == 0) return FMRX_OK;
+    int rc = set_device(c);
+    if (rc) return rc;
+    const size_t ns = c->cfg.n_streams;
+    const size_t in_bytes = ns * n_blocks * c->geo.block_bytes;
+    const size_t n_if = n_blocks * c->geo.if_samples;
+    if ((rc = c->d_in.ensure(in_bytes)) || (rc = c->d_f32.ensure(ns * n_if))) return rc;
+    HIPCHK(hipMemcpyAsync(c->d_in.p, iq, in_bytes, hipMemcpyHostToDevice, c->stream));
+    if ((rc = run_fused(c, c->d_in.p, n_blocks, nullptr, nullptr, c->d_f32.p, n_if, 0, false))) return rc;
+    HIPCHK(hipMemcpyAsync(demod, c->d_f32.p, sizeof(float) * ns * n_if, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return FMRX_OK;
+}
+
+// audio_thread body (project.cpp:132-195): demod floats -> S16.
+int fmrx_audio_block(fmrx_ctx* c, const float* demod, size_t n_blocks, int16_t* pcm) {
+    if (!c || !demod || !pcm) return fail(FMRX_EINVAL, "null argument");
+    if (n_blocks == 0) return FMRX_OK;
+    int rc = set_device(c);
+    if (rc) return rc;
+    const size_t ns = c->cfg.n_streams;
+    const size_t n_if = n_blocks * c->geo.if_samples;
+    const size_t out_n = ns * n_blocks * c->geo.pcm_samples;
+    if ((rc = c->d_out.ensure(out_n))) return rc;
+    if (c->cfg.channels == FMRX_MONO) {
+        if ((rc = c->d_f32.ensure(ns * n_if))) return rc;
+        HIPCHK(hipMemcpyAsync(c->d_f32.p, demod, sizeof(float) * ns * n_if, hipMemcpyHostToDevice, c->stream));
+        if ((rc = run_mono_audio(c, c->d_f32.p, n_if, n_if, c->d_out.p, nullptr))) return rc;
+    } else {
+        if ((rc = ensure_demod(c, n_if))) return rc;
+        HIPCHK(hipMemcpy2DAsync(c->d_demod.p + kDemodHist, c->demod_stride * sizeof(float), demod,
+                                n_if * sizeof(float), n_if * sizeof(float), ns,
+                                hipMemcpyHostToDevice, c->stream));
+        if ((rc = run_stereo_audio(c, n_blocks, c->d_out.p, nullptr))) return rc;
+    }
+    HIPCHK(hipMemcpyAsync(pcm, c->d_out.p, out_n * sizeof(int16_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return FMRX_OK;
+}
+
+// ---- filter.h primitives ---------------------------------------------------------------
+int fmrx_impulse_response_lpf(float* h, float fs, float fc, int taps, int gain) {
+    if (!h || taps < 1) return fail(FMRX_EINVAL, "bad argument");
+    design_lpf(h, fs, fc, taps, gain);
+    return FMRX_OK;
+}
+
+int fmrx_impulse_response_bpf(float* h, float fs, float fb, float fe, int taps) {
+    if (!h || taps < 1) return fail(FMRX_EINVAL, "bad argument");
+    design_bpf(h, fs, fb, fe, taps);
+    return FMRX_OK;
+}
+
+int fmrx_resample(fmrx_ctx* c, float* d_out, float* d_state, const float* d_in, int n_in,
+                  const float* d_coeff, int taps, int up, int down, int* n_out) {
+    if (!c || !d_out || !d_state || !d_in || !d_coeff || taps < 1 || up < 1 || down < 1)
+        return fail(FMRX_EINVAL, "bad argument");
+    if (n_in < taps - 1) return fail(FMRX_EINVAL, "input shorter than the filter history");
+    int rc = set_device(c);
+    if (rc) return rc;
+    const int no = (int)((long long)n_in * up / down);  // filter.cpp:77
+    if (launch_resample(d_out, d_state, d_in, n_in, d_coeff, taps, up, down, no, c->stream) ||
+        launch_tail_copy(d_state, d_in + (n_in - (taps - 1)), taps - 1, c->stream))
+        return fail(FMRX_EHIP, "resample launch failed");
+    if (n_out) *n_out = no;
+    return FMRX_OK;
+}
+
+int fmrx_fm_demod(fmrx_ctx* c, float* d_out, float* d_prev, const float* d_i, const float* d_q, int n) {
+    if (!c || !d_out || !d_prev || !d_i || !d_q || n < 0) return fail(FMRX_EINVAL, "bad argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return launch_fm_demod(d_out, d_prev, d_i, d_q, n, c->stream) ? fail(FMRX_EHIP, "launch failed") : 0;
+}
+
+int fmrx_pll(fmrx_ctx* c, float* d_io, int n, float freq, float fs, float nco_scale, float phase_adjust,
+             float norm_bw, float* d_st) {
+    if (!c || !d_io || !d_st || n < 0) return fail(FMRX_EINVAL, "bad argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    // single stream with a 6-float state: stage through the 8-float layout of the kernel
+    rc = c->d_scratch.ensure(8);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(c->d_scratch.p, d_st, 6 * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
+    if (launch_pll(d_io, n, 1, (size_t)n, freq, fs, nco_scale, phase_adjust, norm_bw, c->d_scratch.p, c->stream))
+        return fail(FMRX_EHIP, "launch failed");
+    HIPCHK(hipMemcpyAsync(d_st, c->d_scratch.p, 6 * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
+    return FMRX_OK;
+}
+
+int fmrx_mixer(fmrx_ctx* c, float* d_out, const float* d_a, const float* d_b, int n) {
+    if (!c || !d_out || !d_a || !d_b || n < 0) return fail(FMRX_EINVAL, "bad argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return launch_mixer(d_out, d_a, d_b, n, c->stream) ? fail(FMRX_EHIP, "launch failed") : 0;
+}
+
+int fmrx_lr_extraction(fmrx_ctx* c, float* d_l, float* d_r, const float* d_m, const float* d_s, int n) {
+    if (!c || !d_l || !d_r || !d_m || !d_s || n < 0) return fail(FMRX_EINVAL, "bad argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return launch_lr(d_l, d_r, d_m, d_s, n, c->stream) ? fail(FMRX_EHIP, "launch failed") : 0;
+}
+
+int fmrx_normalize_iq(fmrx_ctx* c, const uint8_t* d_iq, size_t n_pairs, float* d_i, float* d_q) {
+    if (!c || !d_iq || !d_i || !d_q) return fail(FMRX_EINVAL, "bad argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return launch_normalize(d_iq, n_pairs, d_i, d_q, c->stream) ? fail(FMRX_EHIP, "launch failed") : 0;
+}
+
+int fmrx_quantize(fmrx_ctx* c, const float* d_x, size_t n, int16_t* d_out) {
+    if (!c || !d_x || !d_out) return fail(FMRX_EINVAL, "bad argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return launch_quantize(d_x, n, d_out, c->stream) ? fail(FMRX_EHIP, "launch failed") : 0;
+}
+
+// ---- synthetic input --------------------------------------------------------------------
+int fmrx_synth_host(uint64_t seed, int rf_fs, uint64_t first_pair, size_t n_pairs, uint8_t* out) {
+    if (!out || rf_fs <= 0) return fail(FMRX_EINVAL, "bad argument");
+    SynthParams p;
+    synth_setup(seed, rf_fs, &p);
+    const int16_t* tab = synth_sintab();
+    for (size_t k = 0; k < n_pairs; k++) synth_pair(p, tab, first_pair + k, out + 2 * k);
+    return FMRX_OK;
+}
+
+int fmrx_synth_device(fmrx_ctx* c, uint64_t seed, int rf_fs, uint64_t first_pair, size_t n_pairs,
+                      uint8_t* d_out) {
+    if (!c || !d_out || rf_fs <= 0) return fail(FMRX_EINVAL, "bad argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    SynthParams p;
+    synth_setup(seed, rf_fs, &p);
+    return launch_synth(p, c->d_sintab.p, first_pair, n_pairs, d_out, c->stream)
+               ? fail(FMRX_EHIP, "synth launch failed")
+               : 0;
+}
+
+}  // extern "C"

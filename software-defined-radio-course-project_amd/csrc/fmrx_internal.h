@@ -1,0 +1,107 @@
+// fmrx_internal.h — shared declarations between the host runtime (api.cpp) and the HIP
+// kernels (kernels.hip).  Not part of the public ABI (include/fmrx.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "synth.h"
+
+namespace fmrx {
+
+struct ModeConstants {
+    int rf_fs, rf_decim, if_fs, bp_fs, audio_up, audio_down;
+};
+
+bool mode_constants(int mode, ModeConstants* m);
+void design_lpf(float* h, float fs, float fc, int taps, int gain);
+void design_bpf(float* h, float fs, float fb, float fe, int taps);
+
+constexpr int kMaxRfTaps = 256;
+constexpr int kMonoDelay = 5;   // src/project.cpp:308
+constexpr int kRfFc = 100000;   // src/project.cpp:304
+constexpr int kAudioFc = 16000; // src/project.cpp:305
+
+constexpr int kMaxAudioTaps = 64;
+
+// Coefficient tables handed to kernels by value (kernarg segment -> scalar registers).
+struct MonoTaps {
+    float rf[kMaxRfTaps];
+    float audio[kMaxAudioTaps];
+};
+
+// ---- fused mono receiver (a1 a4 a5 a6 a12; MONO semantics) ---------------------------
+struct MonoLaunch {
+    const uint8_t* iq;          // n_streams x stream_bytes
+    const uint8_t* halo;        // n_streams x halo_bytes: bytes preceding this call
+    int16_t* pcm;               // n_streams x n_blocks*audio_frames
+    float* mono;                // optional float output (same shape), may be null
+    float* demod;               // optional demod output, written at demod[s*demod_stride +
+                                //   demod_hist + g] for IF index g (stereo engine input)
+    size_t demod_stride;
+    int demod_hist;
+    float* demod_tail;          // optional: last audio_taps-1 demod samples, n_streams x AH
+    size_t stream_bytes;        // n_blocks * block_bytes
+    size_t halo_bytes;
+    long long n_if;             // IF samples per stream this call
+    int segs;                   // workgroups (segments) per stream
+    int audio;                  // 1: run the audio stage (pcm / mono outputs)
+};
+
+// Halo bytes the fused kernel needs in front of a call (pre-roll chunk + RF history).
+size_t mono_halo_bytes(int rf_taps, int rf_decim, int audio_down);
+// Chunks (work units) per stream for n_if IF samples, used to size the grid.
+long long mono_chunks(long long n_if, int rf_taps, int rf_decim, int audio_down);
+// Returns 0 on success, FMRX_EINVAL if no compiled variant matches.
+int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_decim,
+                      int audio_down, const MonoTaps& taps, hipStream_t s);
+// Halo bookkeeping: new_halo = last halo_bytes of (old_halo ++ iq), per stream.
+int launch_halo_update(const uint8_t* iq, size_t stream_bytes, const uint8_t* old_halo,
+                       uint8_t* new_halo, size_t halo_bytes, int n_streams, hipStream_t s);
+
+// ---- stereo engine (REF_EXACT) kernels -----------------------------------------------
+struct StereoLaunch {
+    const float* demod;     // n_streams x (hist + n_if): hist demod samples precede each call
+    float* channel;         // n_streams x n_if
+    float* carrier;         // n_streams x n_if (PLL in place -> NCO)
+    int n_if;               // IF samples this call per stream
+    int hist;               // demod history length kept in front (>= taps-1)
+    size_t demod_stride;    // floats between streams in demod
+    const float* ch_c;      // bp taps, HOST memory (passed to the kernel by value)
+    const float* ca_c;
+    int bp_taps;
+};
+int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s);
+int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
+               float nco_scale, float phase_adjust, float norm_bw, float* st, hipStream_t s);
+
+struct AudioLaunch {
+    const float* demod;     // with hist samples in front (per stream stride demod_stride)
+    size_t demod_stride;
+    int hist;
+    const float* channel;   // n_streams x n_if
+    const float* nco;       // n_streams x n_if
+    float* mix_tail;        // n_streams x (at-1): last mixer samples of the previous block
+    float* mono_state;      // n_streams x 5
+    int16_t* pcm;           // n_streams x n_blocks*2*frames
+    float* mono_out;        // optional REF_EXACT mono floats
+    int n_blocks, if_per_block, frames_per_block;
+    int up, down, at;       // audio resampler
+    const float* audio_c;
+};
+int launch_stereo_audio(const AudioLaunch& L, int n_streams, hipStream_t s);
+
+// ---- generic filter.h primitives ------------------------------------------------------
+int launch_resample(float* out, const float* state, const float* in, int n_in,
+                    const float* coeff, int taps, int up, int down, int n_out, hipStream_t s);
+int launch_tail_copy(float* dst, const float* src, int n, hipStream_t s);
+int launch_fm_demod(float* out, float* prev, const float* i, const float* q, int n,
+                    hipStream_t s);
+int launch_mixer(float* out, const float* a, const float* b, int n, hipStream_t s);
+int launch_lr(float* l, float* r, const float* m, const float* st, int n, hipStream_t s);
+int launch_normalize(const uint8_t* iq, size_t n_pairs, float* i, float* q, hipStream_t s);
+int launch_quantize(const float* x, size_t n, int16_t* out, hipStream_t s);
+int launch_synth(const SynthParams& p, const int16_t* d_sintab, uint64_t first, size_t n,
+                 uint8_t* out, hipStream_t s);
+
+}  // namespace fmrx

@@ -1,0 +1,226 @@
+// stereo.hip — the stereo half of the receive chain (src/project.cpp:152-193):
+// channel + carrier band-pass, pilot PLL, mixer, the audio LPF with the reference's SHARED
+// audio_state, the mono delay line, L/R matrix and the R,L S16 quantiser.
+//
+// REF_EXACT semantics: in project.cpp the mono and stereo resample calls of
+// one block share one history vector (project.cpp:114,146,172), so
+//   * mono   of block b uses as history the last samples of block b-1's MIXER output;
+//   * stereo of block b uses as history the last samples of block b's own DEMOD input.
+// Both are reproduced exactly at the reference's block boundaries; this is the only
+// place where the reference block size (SURVEY table M) changes the numbers.
+#include <hip/hip_runtime.h>
+
+#include "dsp_device.h"
+#include "fmrx_internal.h"
+
+namespace fmrx {
+
+namespace {
+
+constexpr double kPi = 3.14159265358979323846;  // include/dy4.h:14
+constexpr int kBpMax = 64;
+
+struct BpTaps {
+    float ch[kBpMax];
+    float ca[kBpMax];
+};
+
+// Channel (22-54 kHz) and carrier (18.5-19.5 kHz) band-pass FIRs share their input, so they
+// run as ONE packed FIR: (acc_ch, acc_ca) += (h_ch[k], h_ca[k]) * x, two exact f32 lanes per
+// v_pk op, each a sequential ascending-k sum (filter.cpp:84-92, up = down = 1).
+template <int BT>
+__global__ void __launch_bounds__(256) bpf_pair_kernel(StereoLaunch L, BpTaps t) {
+    const int s = blockIdx.y;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= L.n_if) return;
+    const float* x = L.demod + (size_t)s * L.demod_stride + L.hist + j;
+    float2v acc = {0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < BT; k++) {
+        const float xv = x[-k];
+        const float2v p = float2v{t.ch[k], t.ca[k]} * xv;
+        acc = acc + p;
+    }
+    L.channel[(size_t)s * L.n_if + j] = acc.x;
+    L.carrier[(size_t)s * L.n_if + j] = acc.y;
+}
+
+__global__ void bpf_pair_generic(StereoLaunch L, BpTaps t) {
+    const int s = blockIdx.y;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= L.n_if) return;
+    const float* x = L.demod + (size_t)s * L.demod_stride + L.hist + j;
+    float a = 0.0f, b = 0.0f;
+    for (int k = 0; k < L.bp_taps; k++) {
+        const float pa = t.ch[k] * x[-k];
+        const float pb = t.ca[k] * x[-k];
+        a = a + pa;
+        b = b + pb;
+    }
+    L.channel[(size_t)s * L.n_if + j] = a;
+    L.carrier[(size_t)s * L.n_if + j] = b;
+}
+
+// src/filter.cpp:136-174 PLL.  A nonlinear recurrence: strictly serial in time, so one lane
+// per stream.  Float state, double-precision atan2 / cos / sin as the reference's libm calls;
+// st = {integrator, phaseEst, feedbackI, feedbackQ, ncoOut_state, trigOffset} (stride 8).
+__global__ void pll_kernel(float* io, int n, int n_streams, size_t stride, float freq, float fs,
+                           float nco_scale, float phase_adjust, float norm_bw, float* st) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_streams) return;
+    float* x = io + (size_t)s * stride;
+    float* S = st + 8 * (size_t)s;
+    const float Cp = static_cast<float>(2.666);
+    const float Ci = static_cast<float>(3.555);
+    const float Kp = norm_bw * Cp;
+    const float Ki = (norm_bw * norm_bw) * Ci;
+    float integ = S[0], phase = S[1], fbI = S[2], fbQ = S[3], trig = S[5];
+    const double step = (2.0 * kPi) * static_cast<double>(freq / fs);
+    for (int i = 0; i < n; i++) {
+        const float v = x[i];
+        const float eI = v * fbI;
+        const float eQ = v * (-fbQ);
+        const float e = static_cast<float>(atan2(static_cast<double>(eQ), static_cast<double>(eI)));
+        integ = integ + Ki * e;
+        phase = phase + ((Kp * e) + integ);
+        trig = trig + 1.0f;
+        const float arg = static_cast<float>(step * static_cast<double>(trig) + static_cast<double>(phase));
+        fbI = static_cast<float>(cos(static_cast<double>(arg)));
+        fbQ = static_cast<float>(sin(static_cast<double>(arg)));
+        x[i] = static_cast<float>(cos(static_cast<double>(arg * nco_scale + phase_adjust)));
+    }
+    S[0] = integ; S[1] = phase; S[2] = fbI; S[3] = fbQ; S[5] = trig;
+    if (n > 0) S[4] = x[n - 1];
+}
+
+// ---- audio stage -------------------------------------------------------------------------
+struct AudioView {
+    const float* d;    // demod of block b (index 0 = first sample of block b)
+    const float* ch;   // channel of block b
+    const float* nco;  // nco of block b
+};
+
+__device__ inline float mixer_at(const AudioView& v, int i) { return 2.0f * (v.ch[i] * v.nco[i]); }
+
+// mono of block b, frame m (project.cpp:146): history = previous block's mixer tail
+// (or the carried tail for the first block of a call).
+__device__ inline float mono_at(const AudioLaunch& L, const AudioView& cur, const AudioView& prv,
+                                bool has_prev, const float* tail, int tl, int m) {
+    const long long nd = (long long)m * L.down;
+    float acc = 0.0f;
+    for (int k = (int)(nd % L.up); k < L.at; k += L.up) {
+        const long long j = (nd - k) / L.up;
+        float x;
+        if (j >= 0) x = cur.d[j];
+        else x = has_prev ? mixer_at(prv, L.if_per_block + (int)j) : tail[tl + j];
+        const float p = L.audio_c[k] * x;
+        acc = acc + p;
+    }
+    return acc;
+}
+
+// stereo of block b, frame m (project.cpp:172): history = the same block's demod tail.
+__device__ inline float stereo_at(const AudioLaunch& L, const AudioView& cur, int m) {
+    const long long nd = (long long)m * L.down;
+    float acc = 0.0f;
+    for (int k = (int)(nd % L.up); k < L.at; k += L.up) {
+        const long long j = (nd - k) / L.up;
+        const float x = j >= 0 ? mixer_at(cur, (int)j) : cur.d[L.if_per_block + j];
+        const float p = L.audio_c[k] * x;
+        acc = acc + p;
+    }
+    return acc;
+}
+
+__device__ inline AudioView view(const AudioLaunch& L, int s, int b) {
+    const size_t nif = (size_t)L.n_blocks * L.if_per_block;
+    AudioView v;
+    v.d = L.demod + (size_t)s * L.demod_stride + L.hist + (size_t)b * L.if_per_block;
+    v.ch = L.channel + (size_t)s * nif + (size_t)b * L.if_per_block;
+    v.nco = L.nco + (size_t)s * nif + (size_t)b * L.if_per_block;
+    return v;
+}
+
+constexpr int kTail = 64;  // mixer tail kept across calls (>= ceil((at-1)/up) + 1)
+
+__global__ void stereo_audio_kernel(AudioLaunch L) {
+    const int s = blockIdx.z;
+    const int b = blockIdx.y;
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= L.frames_per_block) return;
+    const AudioView cur = view(L, s, b);
+    const AudioView prv = b > 0 ? view(L, s, b - 1) : cur;
+    const float* tail = L.mix_tail + (size_t)s * kTail;
+    const float mono = mono_at(L, cur, prv, b > 0, tail, kTail, m);
+    float shift;  // project.cpp:152-159, 5-sample delay line
+    if (m >= kMonoDelay) {
+        shift = mono_at(L, cur, prv, b > 0, tail, kTail, m - kMonoDelay);
+    } else if (b > 0) {
+        const AudioView pp = b > 1 ? view(L, s, b - 2) : prv;
+        shift = mono_at(L, prv, pp, b > 1, tail, kTail, L.frames_per_block - kMonoDelay + m);
+    } else {
+        shift = L.mono_state[(size_t)s * 8 + m];
+    }
+    const float st = stereo_at(L, cur, m);
+    const float left = half_of(shift + st);    // filter.cpp:196
+    const float right = half_of(shift - st);   // filter.cpp:197
+    const size_t o = ((size_t)s * L.n_blocks + b) * (size_t)L.frames_per_block + m;
+    L.pcm[2 * o] = quantize_s16(right);        // project.cpp:184-187 (R first)
+    L.pcm[2 * o + 1] = quantize_s16(left);
+    if (L.mono_out) L.mono_out[o] = mono;
+}
+
+// Carry the audio state of the LAST block of this call into the next call.
+__global__ void stereo_state_kernel(AudioLaunch L) {
+    const int s = blockIdx.x;
+    const int i = threadIdx.x;
+    const int b = L.n_blocks - 1;
+    const AudioView cur = view(L, s, b);
+    const AudioView prv = b > 0 ? view(L, s, b - 1) : cur;
+    const float* tail = L.mix_tail + (size_t)s * kTail;
+    float mono = 0.0f, mix = 0.0f;
+    if (i < kMonoDelay)
+        mono = mono_at(L, cur, prv, b > 0, tail, kTail, L.frames_per_block - kMonoDelay + i);
+    if (i < kTail) mix = mixer_at(cur, L.if_per_block - kTail + i);
+    __syncthreads();  // every read of the old tail happens before it is overwritten
+    if (i < kMonoDelay) L.mono_state[(size_t)s * 8 + i] = mono;
+    if (i < kTail) L.mix_tail[(size_t)s * kTail + i] = mix;
+}
+
+inline int ok() { return hipGetLastError() == hipSuccess ? 0 : -2; }
+
+}  // namespace
+
+int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s) {
+    if (L.n_if <= 0) return 0;
+    if (L.bp_taps > kBpMax) return -1;
+    BpTaps t{};
+    for (int k = 0; k < L.bp_taps; k++) {
+        t.ch[k] = L.ch_c[k];
+        t.ca[k] = L.ca_c[k];
+    }
+    const dim3 grid((L.n_if + 255) / 256, n_streams), block(256);
+    if (L.bp_taps == 51)
+        hipLaunchKernelGGL(bpf_pair_kernel<51>, grid, block, 0, s, L, t);
+    else
+        hipLaunchKernelGGL(bpf_pair_generic, grid, block, 0, s, L, t);
+    return ok();
+}
+
+int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
+               float nco_scale, float phase_adjust, float norm_bw, float* st, hipStream_t s) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(pll_kernel, dim3((n_streams + 63) / 64), dim3(64), 0, s, io, n, n_streams,
+                       stride, freq, fs, nco_scale, phase_adjust, norm_bw, st);
+    return ok();
+}
+
+int launch_stereo_audio(const AudioLaunch& L, int n_streams, hipStream_t s) {
+    if (L.n_blocks <= 0) return 0;
+    const dim3 grid((L.frames_per_block + 127) / 128, L.n_blocks, n_streams);
+    hipLaunchKernelGGL(stereo_audio_kernel, grid, dim3(128), 0, s, L);
+    hipLaunchKernelGGL(stereo_state_kernel, dim3(n_streams), dim3(kTail), 0, s, L);
+    return ok();
+}
+
+}  // namespace fmrx

@@ -1,0 +1,285 @@
+"""fmrx.py — Python host binding of libfmrx.so (the C ABI in include/fmrx.h).
+
+Mirrors the reference's per-block interface (src/project.cpp rf_thread / audio_thread bodies
+and the filter.h primitives) for tests, the bench and Python callers.  There is no CPU
+compute path here: everything numeric runs in the HIP kernels of libfmrx.so, and loading
+fails loudly if the library has not been built.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "libfmrx.so")
+HEADER = os.path.join(REPO, "include", "fmrx.h")
+
+FMRX_OK, FMRX_EINVAL, FMRX_EHIP, FMRX_ENOMEM, FMRX_ESTATE = 0, -1, -2, -3, -4
+MONO, STEREO = 1, 2
+
+
+class FmrxError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"fmrx error {code}: {msg}")
+        self.code = code
+
+
+class Config(C.Structure):
+    _fields_ = [("mode", C.c_int), ("channels", C.c_int), ("rf_taps", C.c_int),
+                ("bp_taps", C.c_int), ("audio_taps", C.c_int), ("n_streams", C.c_int),
+                ("device", C.c_int)]
+
+
+class Geometry(C.Structure):
+    _fields_ = [("rf_fs", C.c_int), ("rf_decim", C.c_int), ("if_fs", C.c_int), ("bp_fs", C.c_int),
+                ("audio_up", C.c_int), ("audio_down", C.c_int), ("rf_taps", C.c_int),
+                ("bp_taps", C.c_int), ("audio_taps_total", C.c_int), ("block_bytes", C.c_size_t),
+                ("iq_pairs", C.c_size_t), ("if_samples", C.c_size_t), ("audio_frames", C.c_size_t),
+                ("pcm_samples", C.c_size_t)]
+
+
+_vp, _sz, _fp, _i16p, _u8p = C.c_void_p, C.c_size_t, C.POINTER(C.c_float), C.POINTER(C.c_int16), C.POINTER(C.c_uint8)
+
+# name -> (restype, argtypes); every function declared in include/fmrx.h
+PROTOTYPES = {
+    "fmrx_config_default": (C.c_int, [C.POINTER(Config), C.c_int, C.c_int]),
+    "fmrx_geometry": (C.c_int, [C.POINTER(Config), C.POINTER(Geometry)]),
+    "fmrx_create": (C.c_int, [C.POINTER(Config), C.POINTER(_vp)]),
+    "fmrx_destroy": (None, [_vp]),
+    "fmrx_reset": (C.c_int, [_vp]),
+    "fmrx_last_error": (C.c_char_p, []),
+    "fmrx_version": (C.c_char_p, []),
+    "fmrx_state_size": (C.c_int, [_vp, C.POINTER(_sz)]),
+    "fmrx_get_state": (C.c_int, [_vp, _vp, _sz]),
+    "fmrx_set_state": (C.c_int, [_vp, _vp, _sz]),
+    "fmrx_process": (C.c_int, [_vp, _vp, _sz, _vp]),
+    "fmrx_rf_block": (C.c_int, [_vp, _vp, _sz, _vp]),
+    "fmrx_audio_block": (C.c_int, [_vp, _vp, _sz, _vp]),
+    "fmrx_process_device": (C.c_int, [_vp, _vp, _sz, _vp]),
+    "fmrx_process_device_ex": (C.c_int, [_vp, _vp, _sz, _vp, _vp]),
+    "fmrx_synchronize": (C.c_int, [_vp]),
+    "fmrx_stream": (_vp, [_vp]),
+    "fmrx_kernel_timing": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_long)]),
+    "fmrx_impulse_response_lpf": (C.c_int, [_fp, C.c_float, C.c_float, C.c_int, C.c_int]),
+    "fmrx_impulse_response_bpf": (C.c_int, [_fp, C.c_float, C.c_float, C.c_float, C.c_int]),
+    "fmrx_resample": (C.c_int, [_vp, _vp, _vp, _vp, C.c_int, _vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int)]),
+    "fmrx_fm_demod": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_int]),
+    "fmrx_pll": (C.c_int, [_vp, _vp, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, _vp]),
+    "fmrx_mixer": (C.c_int, [_vp, _vp, _vp, _vp, C.c_int]),
+    "fmrx_lr_extraction": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_int]),
+    "fmrx_normalize_iq": (C.c_int, [_vp, _vp, _sz, _vp, _vp]),
+    "fmrx_quantize": (C.c_int, [_vp, _vp, _sz, _vp]),
+    "fmrx_synth_host": (C.c_int, [C.c_uint64, C.c_int, C.c_uint64, _sz, _vp]),
+    "fmrx_synth_device": (C.c_int, [_vp, C.c_uint64, C.c_int, C.c_uint64, _sz, _vp]),
+}
+
+_lib = None
+
+
+def header_symbols() -> list[str]:
+    """Function names declared in include/fmrx.h."""
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(fmrx_[a-z0-9_]+)\s*\(", txt)))
+
+
+def lib() -> C.CDLL:
+    """Load libfmrx.so (raises if it is missing: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is not built; run `make -C {PKG_DIR}` "
+                              "(the HIP extension is required, there is no CPU path)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in PROTOTYPES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != FMRX_OK:
+        raise FmrxError(rc, lib().fmrx_last_error().decode())
+
+
+def _np_ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def default_config(mode: int = 0, channels: int = MONO, **kw) -> Config:
+    cfg = Config()
+    _check(lib().fmrx_config_default(C.byref(cfg), mode, channels))
+    for k, v in kw.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+def geometry(cfg: Config) -> Geometry:
+    g = Geometry()
+    _check(lib().fmrx_geometry(C.byref(cfg), C.byref(g)))
+    return g
+
+
+def lpf(fs: float, fc: float, taps: int, gain: int = 1) -> np.ndarray:
+    """impulseResponseLPF (src/filter.cpp:14-37)."""
+    h = np.zeros(taps, np.float32)
+    _check(lib().fmrx_impulse_response_lpf(h.ctypes.data_as(_fp), fs, fc, taps, gain))
+    return h
+
+
+def bpf(fs: float, fb: float, fe: float, taps: int) -> np.ndarray:
+    """impulseResponseBPF (src/filter.cpp:39-64)."""
+    h = np.zeros(taps, np.float32)
+    _check(lib().fmrx_impulse_response_bpf(h.ctypes.data_as(_fp), fs, fb, fe, taps))
+    return h
+
+
+def synth_host(seed: int, rf_fs: int, first_pair: int, n_pairs: int) -> np.ndarray:
+    out = np.zeros(2 * n_pairs, np.uint8)
+    _check(lib().fmrx_synth_host(seed, rf_fs, first_pair, n_pairs, _np_ptr(out)))
+    return out
+
+
+class Receiver:
+    """One libfmrx context: ``n_streams`` independent IQ streams on one GPU.
+
+    Host-buffer methods mirror the reference's block loop; ``*_device`` methods take
+    device pointers (e.g. ``torch.Tensor.data_ptr()``) and enqueue on the context stream.
+    """
+
+    def __init__(self, mode: int = 0, channels: int = MONO, rf_taps: int = 51, n_streams: int = 1,
+                 device: int = 0, bp_taps: int = 51, audio_taps: int = 51):
+        self.cfg = default_config(mode, channels, rf_taps=rf_taps, n_streams=n_streams,
+                                  device=device, bp_taps=bp_taps, audio_taps=audio_taps)
+        self.geo = geometry(self.cfg)
+        h = C.c_void_p()
+        _check(lib().fmrx_create(C.byref(self.cfg), C.byref(h)))
+        self.h = h
+        self.n_streams = n_streams
+        self.channels = channels
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            lib().fmrx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- sizes
+    @property
+    def block_bytes(self) -> int:
+        return self.geo.block_bytes
+
+    def n_blocks(self, n_bytes_per_stream: int) -> int:
+        return n_bytes_per_stream // self.geo.block_bytes
+
+    # ---- host entry points
+    def _streams(self, iq: np.ndarray) -> tuple[np.ndarray, int]:
+        iq = np.ascontiguousarray(iq, np.uint8).reshape(self.n_streams, -1)
+        nb = iq.shape[1] // self.geo.block_bytes
+        return np.ascontiguousarray(iq[:, : nb * self.geo.block_bytes]), nb
+
+    def process(self, iq: np.ndarray) -> np.ndarray:
+        """Full blocks of u8 I/Q (per stream) -> S16 PCM (R,L interleaved for stereo)."""
+        iq, nb = self._streams(iq)
+        out = np.zeros((self.n_streams, nb * self.geo.pcm_samples), np.int16)
+        if nb:
+            _check(lib().fmrx_process(self.h, _np_ptr(iq), nb, _np_ptr(out)))
+        return out if self.n_streams > 1 else out[0]
+
+    def rf_block(self, iq: np.ndarray) -> np.ndarray:
+        """rf_thread body (project.cpp:48-70): u8 I/Q -> demod floats."""
+        iq, nb = self._streams(iq)
+        out = np.zeros((self.n_streams, nb * self.geo.if_samples), np.float32)
+        if nb:
+            _check(lib().fmrx_rf_block(self.h, _np_ptr(iq), nb, _np_ptr(out)))
+        return out if self.n_streams > 1 else out[0]
+
+    def audio_block(self, demod: np.ndarray) -> np.ndarray:
+        """audio_thread body (project.cpp:132-195): demod floats -> S16."""
+        d = np.ascontiguousarray(demod, np.float32).reshape(self.n_streams, -1)
+        nb = d.shape[1] // self.geo.if_samples
+        out = np.zeros((self.n_streams, nb * self.geo.pcm_samples), np.int16)
+        if nb:
+            _check(lib().fmrx_audio_block(self.h, _np_ptr(d), nb, _np_ptr(out)))
+        return out if self.n_streams > 1 else out[0]
+
+    # ---- device entry points (pointers are device addresses)
+    def process_device(self, d_iq: int, n_blocks: int, d_pcm: int, d_mono: int | None = None) -> None:
+        _check(lib().fmrx_process_device_ex(self.h, d_iq, n_blocks, d_pcm, d_mono))
+
+    def synchronize(self) -> None:
+        _check(lib().fmrx_synchronize(self.h))
+
+    def stream(self) -> int:
+        return lib().fmrx_stream(self.h)
+
+    def synth_device(self, seed: int, first_pair: int, n_pairs: int, d_out: int) -> None:
+        _check(lib().fmrx_synth_device(self.h, seed, self.geo.rf_fs, first_pair, n_pairs, d_out))
+
+    def kernel_timing(self, reset: int = 0) -> tuple[float, int]:
+        ms, n = C.c_double(), C.c_long()
+        _check(lib().fmrx_kernel_timing(self.h, reset, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    # ---- state
+    def get_state(self) -> bytes:
+        n = C.c_size_t()
+        _check(lib().fmrx_state_size(self.h, C.byref(n)))
+        buf = (C.c_uint8 * n.value)()
+        _check(lib().fmrx_get_state(self.h, C.addressof(buf), n.value))
+        return bytes(buf)
+
+    def set_state(self, blob: bytes) -> None:
+        buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+        _check(lib().fmrx_set_state(self.h, C.addressof(buf), len(blob)))
+
+    def reset(self) -> None:
+        _check(lib().fmrx_reset(self.h))
+
+    # ---- filter.h primitives on device pointers
+    def resample(self, d_out, d_state, d_in, n_in, d_coeff, taps, up, down) -> int:
+        n = C.c_int()
+        _check(lib().fmrx_resample(self.h, d_out, d_state, d_in, n_in, d_coeff, taps, up, down, C.byref(n)))
+        return n.value
+
+    def fm_demod(self, d_out, d_prev, d_i, d_q, n) -> None:
+        _check(lib().fmrx_fm_demod(self.h, d_out, d_prev, d_i, d_q, n))
+
+    def pll(self, d_io, n, freq, fs, nco_scale, phase_adjust, norm_bw, d_state) -> None:
+        _check(lib().fmrx_pll(self.h, d_io, n, freq, fs, nco_scale, phase_adjust, norm_bw, d_state))
+
+    def mixer(self, d_out, d_a, d_b, n) -> None:
+        _check(lib().fmrx_mixer(self.h, d_out, d_a, d_b, n))
+
+    def lr_extraction(self, d_l, d_r, d_m, d_s, n) -> None:
+        _check(lib().fmrx_lr_extraction(self.h, d_l, d_r, d_m, d_s, n))
+
+    def normalize_iq(self, d_iq, n_pairs, d_i, d_q) -> None:
+        _check(lib().fmrx_normalize_iq(self.h, d_iq, n_pairs, d_i, d_q))
+
+    def quantize(self, d_x, n, d_out) -> None:
+        _check(lib().fmrx_quantize(self.h, d_x, n, d_out))
+
+
+def build() -> None:
+    """Compile libfmrx.so and the fmrx CLI for gfx950 (hipcc cross-compiles without a GPU)."""
+    import subprocess
+
+    subprocess.run(["make", "-s", "-C", PKG_DIR, "-j8"], check=True)

@@ -1,0 +1,300 @@
+"""GPU parity: libfmrx's HIP kernels (through the C ABI) against the reference's outputs.
+
+Every comparison is bit-exact (integer PCM and the float bit patterns of intermediates):
+  * golden fixtures produced by the reference itself (tests/golden, make_golden.py);
+  * the C restatement oracle (pinned to those fixtures) on fresh seeded inputs;
+  * size-independent properties at BASELINE sizes: call-split invariance, state
+    checkpoint/resume, and windowed oracle checks anywhere inside a 1 GiB stream (the mono
+    product has finite memory, so an oracle run started one block early is exact).
+"""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+import iqgen
+import oracle
+from conftest import case_input, golden_cases, load_case, long_runs
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view(np.uint32) if a.dtype == np.float32 else a
+
+
+def same(a, b):
+    return np.array_equal(bits(a), bits(b))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.init()
+
+
+MONO_CASES = [n for n in golden_cases() if "pcm_mono" in load_case(n)]
+STEREO_CASES = [n for n in golden_cases() if "pcm" in load_case(n)]
+
+
+# ---- fused mono product ---------------------------------------------------------------------
+
+@pytest.mark.parametrize("name", MONO_CASES)
+def test_mono_pcm_matches_reference(fmrx, name):
+    z = load_case(name)
+    iq = case_input(z)
+    with fmrx.Receiver(z["mode"], fmrx.MONO, rf_taps=z["rf_taps"]) as rx:
+        pcm = rx.process(iq)
+    assert np.array_equal(pcm, z["pcm_mono"]), name
+
+
+@pytest.mark.parametrize("name", [n for n in MONO_CASES if "mono_indep" in load_case(n)])
+def test_mono_float_matches_reference(fmrx, name):
+    z = load_case(name)
+    iq = case_input(z)
+    with fmrx.Receiver(z["mode"], fmrx.MONO, rf_taps=z["rf_taps"]) as rx:
+        nb = z["n_blocks"]
+        d_iq = torch.from_numpy(iq).cuda()
+        d_pcm = torch.zeros(nb * rx.geo.audio_frames, dtype=torch.int16, device="cuda")
+        d_mono = torch.zeros(nb * rx.geo.audio_frames, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        rx.process_device(d_iq.data_ptr(), nb, d_pcm.data_ptr(), d_mono.data_ptr())
+        rx.synchronize()
+        assert same(d_mono.cpu().numpy(), z["mono_indep"])
+        assert np.array_equal(d_pcm.cpu().numpy(), z["pcm_mono"])
+
+
+@pytest.mark.parametrize("name", [n for n in golden_cases() if "demod" in load_case(n)])
+def test_rf_block_demod_matches_reference(fmrx, name):
+    z = load_case(name)
+    with fmrx.Receiver(z["mode"], fmrx.MONO, rf_taps=z["rf_taps"]) as rx:
+        demod = rx.rf_block(case_input(z))
+    assert same(demod, z["demod"])
+
+
+@pytest.mark.parametrize("name", [n for n in MONO_CASES if "demod" in load_case(n)])
+def test_mono_audio_block_from_reference_demod(fmrx, name):
+    z = load_case(name)
+    with fmrx.Receiver(z["mode"], fmrx.MONO, rf_taps=z["rf_taps"]) as rx:
+        pcm = rx.audio_block(z["demod"])
+    assert np.array_equal(pcm, z["pcm_mono"])
+
+
+@pytest.mark.parametrize("mode,rf_taps", [(0, 51), (0, 101), (1, 51), (1, 101)])
+def test_mono_call_split_and_resume(fmrx, orc, mode, rf_taps):
+    bb, rf_fs = oracle.MODES[mode][0], oracle.MODES[mode][3]
+    nb = 37
+    iq = iqgen.make("synth:41", nb * bb, rf_fs)
+    want = orc.run(mode, rf_taps, iq, ["pcm_mono"])["pcm_mono"]
+    with fmrx.Receiver(mode, fmrx.MONO, rf_taps=rf_taps) as rx:
+        got = rx.process(iq)
+        assert np.array_equal(got, want)
+        rx.reset()
+        parts, pos = [], 0
+        na = rx.geo.audio_frames
+        for n in (1, 2, 5, 1, 11, 3, 14):  # ragged call sizes, 37 blocks in total
+            parts.append(rx.process(iq[pos * bb:(pos + n) * bb]))
+            pos += n
+            if pos == 9:  # checkpoint / resume through a second context
+                blob = rx.get_state()
+                with fmrx.Receiver(mode, fmrx.MONO, rf_taps=rf_taps) as rx2:
+                    rx2.set_state(blob)
+                    tail = rx2.process(iq[pos * bb:])
+                assert np.array_equal(tail, want[pos * na:])
+        assert np.array_equal(np.concatenate(parts), want)
+
+
+def test_mono_multistream_independent(fmrx, orc):
+    nb, bb = 23, 12800
+    ins = [iqgen.make(r, nb * bb) for r in ("synth:51", "rand:52", "synth:53", "const128")]
+    with fmrx.Receiver(0, fmrx.MONO, rf_taps=101, n_streams=len(ins)) as rx:
+        out = rx.process(np.stack(ins))
+    for s, iq in enumerate(ins):
+        assert np.array_equal(out[s], orc.run(0, 101, iq, ["pcm_mono"])["pcm_mono"]), s
+
+
+def test_partial_block_dropped_and_empty(fmrx, orc):
+    iq = iqgen.make("synth:55", 3 * 12800 + 5000)
+    with fmrx.Receiver(0, fmrx.MONO) as rx:
+        assert rx.process(iq[:1000]).size == 0
+        rx.reset()
+        got = rx.process(iq)
+    assert np.array_equal(got, orc.run(0, 51, iq, ["pcm_mono"])["pcm_mono"])
+
+
+@pytest.mark.parametrize("name", [n for n in long_runs() if long_runs()[n]["mode"] in (0, 1)])
+def test_mono_long_hash(fmrx, name):
+    h = long_runs()[name]
+    bb, rf_fs = oracle.MODES[h["mode"]][0], oracle.MODES[h["mode"]][3]
+    iq = iqgen.make(h["recipe"], h["n_blocks"] * bb, rf_fs)
+    with fmrx.Receiver(h["mode"], fmrx.MONO, rf_taps=h["rf_taps"]) as rx:
+        assert sha(rx.process(iq)) == h["pcm_mono_sha256"]
+
+
+def test_full_size_1gib_windowed(fmrx, orc):
+    """BASELINE config 2 at full size: 1 GiB of synthetic I/Q, 101-tap RF, mono.  The GPU
+    generates the bytes; windows anywhere in the output are checked bit-exactly against the
+    oracle run on that window's bytes (started one block early: finite filter memory)."""
+    nbytes = 1 << 30
+    bb, na = 12800, 128
+    nb = nbytes // bb
+    with fmrx.Receiver(0, fmrx.MONO, rf_taps=101) as rx:
+        d_iq = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        d_pcm = torch.empty(nb * na, dtype=torch.int16, device="cuda")
+        torch.cuda.synchronize()
+        rx.synth_device(77, 0, nbytes // 2, d_iq.data_ptr())
+        rx.process_device(d_iq.data_ptr(), nb, d_pcm.data_ptr())
+        rx.synchronize()
+        pcm = d_pcm.cpu().numpy()
+        rng = np.random.default_rng(0)
+        for b in [0, 1, 2, nb // 2, nb - 2, nb - 1] + list(rng.integers(1, nb - 1, 10)):
+            b0 = max(0, int(b) - 1)
+            win = d_iq[b0 * bb:(int(b) + 1) * bb].cpu().numpy()
+            assert np.array_equal(win, iqgen.load_fmrx().synth_host(77, 2400000, b0 * bb // 2, win.size // 2))
+            want = orc.run(0, 101, win, ["pcm_mono"])["pcm_mono"][(int(b) - b0) * na:]
+            assert np.array_equal(pcm[int(b) * na:(int(b) + 1) * na], want), b
+
+
+# ---- stereo engine (project.cpp output) -----------------------------------------------------
+
+@pytest.mark.parametrize("name", STEREO_CASES)
+def test_stereo_pcm_matches_reference(fmrx, name):
+    z = load_case(name)
+    iq = case_input(z)
+    with fmrx.Receiver(z["mode"], fmrx.STEREO, rf_taps=z["rf_taps"]) as rx:
+        nb = z["n_blocks"]
+        d_iq = torch.from_numpy(iq).cuda()
+        d_pcm = torch.zeros(nb * rx.geo.pcm_samples, dtype=torch.int16, device="cuda")
+        d_mono = torch.zeros(nb * rx.geo.audio_frames, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        rx.process_device(d_iq.data_ptr(), nb, d_pcm.data_ptr(), d_mono.data_ptr())
+        rx.synchronize()
+        pcm = d_pcm.cpu().numpy()
+        if "mono_exact" in z:
+            assert same(d_mono.cpu().numpy(), z["mono_exact"]), "REF_EXACT mono differs"
+    assert np.array_equal(pcm, z["pcm"]), name
+
+
+@pytest.mark.parametrize("name", [n for n in STEREO_CASES if "demod" in load_case(n)])
+def test_stereo_audio_block_from_reference_demod(fmrx, name):
+    z = load_case(name)
+    with fmrx.Receiver(z["mode"], fmrx.STEREO, rf_taps=z["rf_taps"]) as rx:
+        pcm = rx.audio_block(z["demod"])
+    assert np.array_equal(pcm, z["pcm"])
+
+
+def test_stereo_call_split(fmrx, orc):
+    nb, bb = 19, 12800
+    iq = iqgen.make("synth:61", nb * bb)
+    want = orc.run(0, 51, iq, ["pcm"])["pcm"]
+    with fmrx.Receiver(0, fmrx.STEREO) as rx:
+        parts, pos = [], 0
+        for n in (1, 4, 2, 9, 3):
+            parts.append(rx.process(iq[pos * bb:(pos + n) * bb]))
+            pos += n
+    assert np.array_equal(np.concatenate(parts), want)
+
+
+def test_stereo_multistream(fmrx, orc):
+    nb, bb = 9, 12800
+    ins = [iqgen.make(f"synth:{70 + s}", nb * bb) for s in range(5)]
+    with fmrx.Receiver(0, fmrx.STEREO, n_streams=5) as rx:
+        out = rx.process(np.stack(ins))
+    for s, iq in enumerate(ins):
+        assert np.array_equal(out[s], orc.run(0, 51, iq, ["pcm"])["pcm"]), s
+
+
+@pytest.mark.parametrize("name", sorted(long_runs()))
+def test_stereo_long_hash(fmrx, name):
+    h = long_runs()[name]
+    bb, rf_fs = oracle.MODES[h["mode"]][0], oracle.MODES[h["mode"]][3]
+    iq = iqgen.make(h["recipe"], h["n_blocks"] * bb, rf_fs)
+    with fmrx.Receiver(h["mode"], fmrx.STEREO, rf_taps=h["rf_taps"]) as rx:
+        assert sha(rx.process(iq)) == h["pcm_sha256"]
+
+
+def test_mode2_mono_long_hash(fmrx):
+    h = long_runs()["m2_rf51_synth_4s"]
+    iq = iqgen.make(h["recipe"], h["n_blocks"] * 2048000, 2400000)
+    with fmrx.Receiver(2, fmrx.MONO) as rx:
+        assert sha(rx.process(iq)) == h["pcm_mono_sha256"]
+
+
+# ---- filter.h primitives --------------------------------------------------------------------
+
+def _d(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def test_primitives(fmrx, taps_golden):
+    g = taps_golden
+    with fmrx.Receiver(0, fmrx.MONO) as rx:
+        c = _d(g["rf_m0_51"])
+        for up, down in ((1, 10), (1, 1), (3, 7)):
+            x, st = _d(g["resample_in"]), _d(g["resample_state"])
+            out = torch.zeros(1000 * up // down, dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            n = rx.resample(out.data_ptr(), st.data_ptr(), x.data_ptr(), 1000, c.data_ptr(), 51, up, down)
+            rx.synchronize()
+            assert n == out.numel()
+            assert same(out.cpu().numpy(), g[f"resample_{up}_{down}_out"])
+            assert same(st.cpu().numpy(), g[f"resample_{up}_{down}_state"])
+        i, q, prev = _d(g["demod_i"]), _d(g["demod_q"]), _d(np.array([0.25, -0.5], np.float32))
+        out = torch.zeros(600, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        rx.fm_demod(out.data_ptr(), prev.data_ptr(), i.data_ptr(), q.data_ptr(), 600)
+        rx.synchronize()
+        assert same(out.cpu().numpy(), g["demod_out"]) and same(prev.cpu().numpy(), g["demod_prev"])
+        io, st = _d(g["pll_in"]), _d(np.array([0, 0, 1, 0, 1, 0], np.float32))
+        torch.cuda.synchronize()
+        rx.pll(io.data_ptr(), io.numel(), 19000, 240000, 2, 0, 0.01, st.data_ptr())
+        rx.synchronize()
+        assert same(io.cpu().numpy(), g["pll_out"]) and same(st.cpu().numpy(), g["pll_state"])
+        b = _d(g["norm_in"])
+        fi = torch.zeros(256, dtype=torch.float32, device="cuda")
+        fq = torch.zeros(256, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        rx.normalize_iq(b.data_ptr(), 256, fi.data_ptr(), fq.data_ptr())
+        rx.synchronize()
+        assert same(fi.cpu().numpy(), g["norm_out"][0::2]) and same(fq.cpu().numpy(), g["norm_out"][1::2])
+
+
+def test_quantize_and_elementwise(fmrx, orc):
+    x = np.array([0, 1, -1, 1.99993896484375, 2, -2, 2.5, 1e6, -1e6, 1.4e5, np.inf, -np.inf, np.nan,
+                  131071.99, -131072, 3.05e-5] * 4, np.float32)
+    with fmrx.Receiver(0, fmrx.MONO) as rx:
+        dx = _d(x)
+        dq = torch.zeros(x.size, dtype=torch.int16, device="cuda")
+        a, b = _d(x[::-1].copy()), _d(np.nan_to_num(x))
+        mix = torch.zeros(x.size, dtype=torch.float32, device="cuda")
+        l = torch.zeros_like(mix)
+        r = torch.zeros_like(mix)
+        torch.cuda.synchronize()
+        rx.quantize(dx.data_ptr(), x.size, dq.data_ptr())
+        rx.mixer(mix.data_ptr(), a.data_ptr(), b.data_ptr(), x.size)
+        rx.lr_extraction(l.data_ptr(), r.data_ptr(), a.data_ptr(), b.data_ptr(), x.size)
+        rx.synchronize()
+    assert np.array_equal(dq.cpu().numpy(), orc.quant(x))
+    xa, xb = x[::-1].copy(), np.nan_to_num(x)
+    assert same(mix.cpu().numpy(), (np.float32(2) * (xa * xb)).astype(np.float32))
+    assert same(l.cpu().numpy(), ((xa + xb).astype(np.float64) * 0.5).astype(np.float32))
+    assert same(r.cpu().numpy(), ((xa - xb).astype(np.float64) * 0.5).astype(np.float32))
+
+
+def test_device_synth_equals_host(fmrx):
+    with fmrx.Receiver(0, fmrx.MONO) as rx:
+        d = torch.empty(2 * 300001, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        rx.synth_device(9, 123456, 300001, d.data_ptr())
+        rx.synchronize()
+        assert np.array_equal(d.cpu().numpy(), fmrx.synth_host(9, 2400000, 123456, 300001))
