@@ -109,7 +109,7 @@ namespace {
 
 bool fused_rf_supported(const fmrx_ctx* c) {
     const int t = c->geo.rf_taps, d = c->geo.rf_decim;
-    return (t == 51 || t == 101) && (d == 10 || d == 4);
+    return (t == 51 || t == 101) && (d == 10 || d == 4 || d == 9);
 }
 
 int set_device(const fmrx_ctx* c) {
@@ -145,7 +145,7 @@ int reset_state(fmrx_ctx* c) {
 // dominates.
 int mono_segments(const fmrx_ctx* c, long long n_if) {
     const long long chunks = mono_chunks(n_if, c->geo.rf_taps, c->geo.rf_decim, c->geo.audio_down);
-    const long long target_wg = 512;
+    const long long target_wg = 256LL * mono_wg_per_cu(c->geo.rf_decim);  // one full wave of workgroups
     long long segs = std::max<long long>(1, target_wg / std::max(1, c->cfg.n_streams));
     segs = std::min(segs, std::max<long long>(1, chunks / 4));
     return (int)std::max<long long>(1, segs);

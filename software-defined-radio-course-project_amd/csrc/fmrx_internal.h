@@ -52,6 +52,8 @@ struct MonoLaunch {
 size_t mono_halo_bytes(int rf_taps, int rf_decim, int audio_down);
 // Chunks (work units) per stream for n_if IF samples, used to size the grid.
 long long mono_chunks(long long n_if, int rf_taps, int rf_decim, int audio_down);
+// Resident workgroups per CU of the selected variant (grid sizing).
+int mono_wg_per_cu(int rf_decim);
 // Returns 0 on success, FMRX_EINVAL if no compiled variant matches.
 int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_decim,
                       int audio_down, const MonoTaps& taps, hipStream_t s);

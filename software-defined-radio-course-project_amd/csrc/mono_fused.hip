@@ -30,6 +30,9 @@
 //   audio : 51-tap decimating LPF over the demod window in LDS, quantise, store S16.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "dsp_device.h"
 #include "fmrx_internal.h"
 
@@ -48,61 +51,62 @@ struct MonoCfg {
     static constexpr int P = CIF * D;                   // I/Q pairs per chunk
     static constexpr int H = T - 1;                     // RF history pairs
     static constexpr int WH = T - 1 + D * (R - 1);      // highest window offset of a thread
-    // LDS slot of buffer pair b (b = H + chunk-relative pair).  The +1 shift and the pad
-    // placement make every (odd o, o+1) window pair one aligned 16-B ds_read_b128 that never
-    // straddles a pad, and make the lane stride (S+G) pairs bank-conflict free.
-    static constexpr int pad(int b) { return b + G * ((b + 1) / S); }
-    static constexpr int slot(int b) { return pad(b) + 1; }
-    static constexpr int XB = slot(H + P + 2) + 2;      // LDS pairs
-    static constexpr int NL = (2 * P / 16 + NT - 1) / NT;  // 16-B loads per thread per chunk
-    static constexpr int CAmax = (CIF + AD - 1) / AD + 1;  // audio outputs per chunk (bound)
-    static_assert(T % 2 == 1, "odd tap count (window pairs align on odd offsets)");
-    static_assert(D % 2 == 0 && S % 2 == 0, "even decimation keeps pair groups aligned");
-    static_assert((2 * P) % 16 == 0, "chunk must be a whole number of 16-B loads");
+    // LDS slot of buffer pair b (b = H + chunk-relative pair).  Pads of G pairs every S pairs
+    // make the lane stride (S+G) pairs bank-conflict free for ds_read_b128, and (even b, b+1)
+    // groups never straddle a pad, so every pair group is one aligned 16-B access.
+    static constexpr int slot(int b) { return b + G * (b / S); }
+    static constexpr int XB = slot(H + P + 2) + 4;      // LDS pairs
+    static constexpr int NLD = (P / 2 + NT - 1) / NT;   // 4-B (2-pair) loads per thread/chunk
+    static constexpr int CAmax = (CIF + AD - 1) / AD;   // max audio outputs in one chunk
+    static constexpr int NG = (T + 1) / 2;              // tap groups: {0}, {1,2}, {3,4}, ...
+    static_assert(T % 2 == 1, "odd tap count");
+    static_assert(S % 2 == 0 && H % 2 == 0, "pair groups must stay 16-B aligned");
+    static_assert(P % 2 == 0, "chunk must be whole dwords");
     static_assert(CAmax <= NT, "one audio output per thread per chunk");
 };
 
-// 16 bytes of the virtual stream (halo ++ data ++ 0x80 padding) at byte offset `off`
-// (a multiple of 16).  Bytes past the end read as 128, i.e. x = 0.0.
-__device__ inline uint4 load16(const uint8_t* in, const uint8_t* halo, long long off,
-                               long long total, long long halo_bytes) {
+// 4 bytes (two I/Q pairs) of the virtual stream (halo ++ data ++ 0x80 padding) at byte
+// offset `off` (a multiple of 4).  Bytes past the end read as 128, i.e. x = 0.0.
+__device__ inline uint32_t load4(const uint8_t* in, const uint8_t* halo, long long off,
+                                 long long total, long long halo_bytes) {
     if (off >= 0) {
-        if (off + 16 <= total) return *reinterpret_cast<const uint4*>(in + off);
-        return make_uint4(0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u);
+        if (off + 4 <= total) return *reinterpret_cast<const uint32_t*>(in + off);
+        return 0x80808080u;
     }
-    return *reinterpret_cast<const uint4*>(halo + (halo_bytes + off));
+    return *reinterpret_cast<const uint32_t*>(halo + (halo_bytes + off));
 }
 
-__device__ inline uint32_t load_pair(const uint8_t* in, const uint8_t* halo, long long pair,
-                                     long long total, long long halo_bytes) {
-    const long long off = 2 * pair;
-    const uint8_t* p;
-    if (off >= 0) {
-        if (off + 2 > total) return 0x8080u;
-        p = in + off;
-    } else {
-        p = halo + (halo_bytes + off);
-    }
-    return (uint32_t)p[0] | ((uint32_t)p[1] << 8);
+// Signed sample of byte k of w after w ^= 0x80808080: s = u - 128 as an exact float.  One
+// SDWA v_cvt_f32_i32 with sign extension per sample.  The FIR runs on s (the reference's
+// x = s / 128): fl(c*s) * 2^-7 == fl(c*x) and every partial sum scales exactly too (all
+// values stay far from the subnormal range), so the 2^-7 is applied once per output.
+template <int K>
+__device__ inline float sbyte(uint32_t w) {
+    float f;
+    if constexpr (K == 0)
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0" : "=v"(f) : "v"(w));
+    else if constexpr (K == 1)
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1" : "=v"(f) : "v"(w));
+    else if constexpr (K == 2)
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2" : "=v"(f) : "v"(w));
+    else
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3" : "=v"(f) : "v"(w));
+    return f;
 }
 
-__device__ inline float2v byte_pair(uint32_t w) {
-    return float2v{u8_to_sample(w & 0xFFu), u8_to_sample((w >> 8) & 0xFFu)};
-}
-
-template <int T, int D, int AD, int NT, int R>
+template <int T, int D, int AD, int NT, int R, int PD>
 __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps taps) {
     using C = MonoCfg<T, D, AD, NT, R>;
-    constexpr int CIF = C::CIF, P = C::P, H = C::H, S = C::S, G = C::G, NL = C::NL;
-    constexpr int WH = C::WH;
+    constexpr int CIF = C::CIF, P = C::P, H = C::H, S = C::S, G = C::G, NLD = C::NLD;
+    constexpr int WH = C::WH, NG = C::NG;
 
-    __shared__ float4 xb4[C::XB / 2 + 1];        // (I,Q) pairs, two per float4
+    __shared__ float4 xb4[C::XB / 2 + 1];        // scaled (I,Q) pairs, two per float4
     __shared__ float dbuf[2][kAH + CIF];         // demod window: 50 history + chunk
     __shared__ float2v pbuf[2][NT + 1];          // last RF output of each thread (+carry)
-    __shared__ float4 ctab4[(T + 3) / 4 + 1];    // RF taps (broadcast reads)
+    __shared__ float2 ctab2[NG + 1];             // (c[2j-1], c[2j]); c[-1] = 0
     __shared__ float atab[kAudioTaps + 1];       // audio taps
     float2v* xb = reinterpret_cast<float2v*>(xb4);
-    float* ctab = reinterpret_cast<float*>(ctab4);
+    float* ctab = reinterpret_cast<float*>(ctab2);
 
     const int tid = threadIdx.x;
     const int stream = blockIdx.x / L.segs;
@@ -119,91 +123,93 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     const long long total = (long long)L.stream_bytes;
     const long long hb = (long long)L.halo_bytes;
 
-    for (int i = tid; i < 4 * ((T + 3) / 4 + 1); i += NT) ctab[i] = i < T ? taps.rf[i] : 0.0f;
+    for (int i = tid; i < 2 * (NG + 1); i += NT) ctab[i] = (i >= 1 && i <= T) ? taps.rf[i - 1] : 0.0f;
     for (int i = tid; i < kAudioTaps; i += NT) atab[i] = taps.audio[i];
 
     // ---- prologue: RF history in front of the pre-roll chunk (pairs [(c0-1)P - H, (c0-1)P))
-    {
-        const long long p0 = (c0 - 1) * (long long)P - H;
-        for (int i = tid; i < H; i += NT) xb[C::slot(i)] = byte_pair(load_pair(in, halo, p0 + i, total, hb));
+    for (int i = tid; i < H / 2; i += NT) {
+        const uint32_t w = load4(in, halo, ((c0 - 1) * (long long)P - H + 2 * i) * 2, total, hb) ^ 0x80808080u;
+        xb4[C::slot(2 * i) / 2] = make_float4(sbyte<0>(w), sbyte<1>(w), sbyte<2>(w), sbyte<3>(w));
     }
-    uint4 pf[NL];
+    uint32_t pf[NLD];
 #pragma unroll
-    for (int l = 0; l < NL; l++) {
+    for (int l = 0; l < NLD; l++) {
         const int u = tid + l * NT;
-        if (u < 2 * P / 16) pf[l] = load16(in, halo, (c0 - 1) * 2LL * P + 16LL * u, total, hb);
+        if (u < P / 2) pf[l] = load4(in, halo, (c0 - 1) * 2LL * P + 4LL * u, total, hb);
     }
 
     int cur = 0;
     for (long long c = c0 - 1; c < c1; c++) {
-        // ---- stage chunk c: 16 B = 8 pairs b0..b0+7 (b0 = H + 8u even) -> LDS slots.
-        // slot(b) is odd for even b, so the group is written as b0 | b0+1..b0+6 | b0+7.
+        // ---- stage chunk c: lane u writes pairs H+2u, H+2u+1 as one float4; consecutive
+        // lanes write consecutive 16-B slots (conflict-free ds_write_b128).
 #pragma unroll
-        for (int l = 0; l < NL; l++) {
+        for (int l = 0; l < NLD; l++) {
             const int u = tid + l * NT;
-            if (u < 2 * P / 16) {
-                const int b0 = H + 8 * u;
-                const uint32_t w[4] = {pf[l].x, pf[l].y, pf[l].z, pf[l].w};
-                float v[16];
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    v[4 * q + 0] = u8_to_sample(w[q] & 0xFFu);
-                    v[4 * q + 1] = u8_to_sample((w[q] >> 8) & 0xFFu);
-                    v[4 * q + 2] = u8_to_sample((w[q] >> 16) & 0xFFu);
-                    v[4 * q + 3] = u8_to_sample(w[q] >> 24);
-                }
-                xb[C::slot(b0)] = float2v{v[0], v[1]};
-#pragma unroll
-                for (int q = 0; q < 3; q++)
-                    xb4[C::slot(b0 + 1 + 2 * q) / 2] =
-                        make_float4(v[2 + 4 * q], v[3 + 4 * q], v[4 + 4 * q], v[5 + 4 * q]);
-                xb[C::slot(b0 + 7)] = float2v{v[14], v[15]};
+            if ((P / 2) % NT == 0 || u < P / 2) {
+                const uint32_t w = pf[l] ^ 0x80808080u;
+                xb4[C::slot(H + 2 * u) / 2] = make_float4(sbyte<0>(w), sbyte<1>(w), sbyte<2>(w), sbyte<3>(w));
             }
         }
         __syncthreads();  // (A) chunk c staged, carry from c-1 in place
         if (c + 1 < c1) {
+            const long long nb0 = (c + 1) * 2LL * P;  // first byte of chunk c+1
+            if (nb0 + 2LL * P <= total) {
+                // interior chunk (all but the last of a stream): plain coalesced dword loads
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(in + nb0) + tid;
 #pragma unroll
-            for (int l = 0; l < NL; l++) {
-                const int u = tid + l * NT;
-                if (u < 2 * P / 16) pf[l] = load16(in, halo, (c + 1) * 2LL * P + 16LL * u, total, hb);
+                for (int l = 0; l < NLD; l++)
+                    if ((P / 2) % NT == 0 || tid + l * NT < P / 2) pf[l] = src[l * NT];
+            } else {
+#pragma unroll
+                for (int l = 0; l < NLD; l++) {
+                    const int u = tid + l * NT;
+                    if (u < P / 2) pf[l] = load4(in, halo, nb0 + 4LL * u, total, hb);
+                }
             }
         }
 
         // ---- RF LPF + decimate.  Thread t owns outputs j = R t + r, r < R, whose samples are
         // window offsets o = D r + T-1-k (window base pair S t).  Tap-outer order: at tap k all
         // R outputs take their k-th term, so each output is still an ascending-k sequential
-        // sum, while the samples slide through a register window (each LDS pair read once) and
-        // each tap is one broadcast LDS value.
+        // sum, while samples slide through a register window (each LDS pair read once per
+        // thread) and taps come as broadcast LDS pairs.  Group 0 = tap 0, group j = taps
+        // 2j-1, 2j; group j's new samples are the pair (T-1-2j, T-2j); loads run PD groups
+        // ahead of use.
         float2v acc[R];
 #pragma unroll
         for (int r = 0; r < R; r++) acc[r] = float2v{0.0f, 0.0f};
         int zero;  // opaque 0: keeps the tap reads as one base VGPR + immediate offsets
         asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
-        const float* cbase = ctab + zero;
-        float2v X[WH + 2];  // X[o + 1] = window pair o, o in [-1, WH]
-        // slot(S t + o) = (S+G) t + o + 1 + G*((o+1)/S): a per-thread base plus a compile-time
-        // offset, so every read is ds_read_b128 base, offset:imm.
+        const float2* cb = ctab2 + zero;
+        float2v X[WH + 3];  // X[o] = window pair o, o in [0, WH+1]
+        float2 cc[NG];
         const float4* wb = xb4 + ((S + G) / 2) * tid;
-        auto ld = [&](int o) {  // o odd: pairs (o, o+1) in one ds_read_b128
-            const float4 q = wb[(o + 1 + G * ((o + 1) / S)) / 2];
-            X[o + 1] = float2v{q.x, q.y};
-            X[o + 2] = float2v{q.z, q.w};
+        auto ld = [&](int o) {  // o even: pairs (o, o+1), one ds_read_b128
+            const float4 q = wb[(o + G * (o / S)) / 2];
+            X[o] = float2v{q.x, q.y};
+            X[o + 1] = float2v{q.z, q.w};
+        };
+        auto ldg = [&](int j) {  // loads of group j
+            if (j < NG) {
+                cc[j] = cb[j];
+                if (j >= 1) ld(T - 1 - 2 * j);
+            }
         };
 #pragma unroll
-        for (int o = WH - 1; o >= T; o -= 2) ld(o);
-        ld(T - 2);
-        ld(T - 4);
+        for (int o = T - 1; o <= WH; o += 2) ld(o);
 #pragma unroll
-        for (int k = 0; k < T; k += 2) {
-            if (T - 6 - k >= -1) ld(T - 6 - k);  // two steps of prefetch distance
-            const float2 cc = *reinterpret_cast<const float2*>(&cbase[k]);
+        for (int j = 0; j < PD; j++) ldg(j);
+#pragma unroll
+        for (int j = 0; j < NG; j++) {
+            ldg(j + PD);
 #pragma unroll
             for (int h = 0; h < 2; h++) {
-                if (k + h < T) {
-                    const float ck = h == 0 ? cc.x : cc.y;
+                const int k = 2 * j - 1 + h;
+                if (k >= 0) {
+                    const float ck = h == 0 ? cc[j].x : cc[j].y;
 #pragma unroll
                     for (int r = 0; r < R; r++) {
-                        const float2v p = X[T - 1 - (k + h) + D * r + 1] * ck;
+                        const float2v p = X[T - 1 - k + D * r] * ck;
                         acc[r] = acc[r] + p;
                     }
                 }
@@ -213,7 +219,10 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         // Pin the accumulators here: without it LLVM sinks the pure-register FIR chains past
         // the barrier to their first use (demod), keeping the whole sample window live.
 #pragma unroll
-        for (int r = 0; r < R; r++) asm volatile("" ::"v"(acc[r]));
+        for (int r = 0; r < R; r++) {
+            asm volatile("" ::"v"(acc[r]));
+            acc[r] = acc[r] * 0.0078125f;  // undo the 2^7 sample scaling (exact)
+        }
         pbuf[cur][tid + 1] = acc[R - 1];
         __syncthreads();  // (B) all RF reads of xb done, pbuf visible
 
@@ -271,39 +280,70 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     }
 }
 
-template <int T, int D, int AD, int NT, int R>
+template <int T, int D, int AD, int NT, int R, int PD>
 int launch_variant(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStream_t s) {
     const dim3 grid(n_streams * L.segs), block(NT);
-    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R>), grid, block, 0, s, L, taps);
+    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD>), grid, block, 0, s, L, taps);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-// Tunables per (decim, audio_down) family.
-constexpr int kNT = 256;
-constexpr int kR = 3;
+// Tunables.  The default was picked by measurement on MI355X (tools/tune_mono.py); other
+// variants stay compiled for the tuning sweep (FMRX_MONO_VARIANT=<index>).
+struct Variant {
+    int nt, r, pd, wg_per_cu;  // wg_per_cu: resident workgroups per CU (LDS-limited)
+};
+constexpr Variant kVariants[] = {{256, 3, 3, 2}, {128, 3, 3, 4}, {64, 3, 3, 8}, {128, 5, 3, 3},
+                                 {256, 3, 5, 2}};
+constexpr int kDefaultVariant = 2;  // 64-thread workgroups: waves never wait on each other
+
+int variant_index() {
+    static int v = [] {
+        const char* e = getenv("FMRX_MONO_VARIANT");
+        const int i = e ? atoi(e) : kDefaultVariant;
+        return (i >= 0 && i < (int)(sizeof kVariants / sizeof kVariants[0])) ? i : kDefaultVariant;
+    }();
+    return v;
+}
 
 }  // namespace
 
 size_t mono_halo_bytes(int rf_taps, int rf_decim, int /*audio_down*/) {
-    const size_t pairs = (size_t)kNT * kR * rf_decim + (size_t)(rf_taps - 1);
+    size_t pairs = 0;  // the largest pre-roll chunk over all variants + RF history
+    for (const Variant& v : kVariants) pairs = std::max(pairs, (size_t)v.nt * v.r * rf_decim);
+    pairs += (size_t)(rf_taps - 1);
     return ((2 * pairs + 15) / 16) * 16 + 16;
 }
 
-long long mono_chunks(long long n_if, int /*rf_taps*/, int /*rf_decim*/, int /*audio_down*/) {
-    const long long cif = (long long)kNT * kR;
+long long mono_chunks(long long n_if, int /*rf_taps*/, int rf_decim, int /*audio_down*/) {
+    const Variant v = kVariants[variant_index()];
+    const long long cif = rf_decim == 9 ? 64 * 2 : (long long)v.nt * v.r;
     return (n_if + cif - 1) / cif;
 }
 
+int mono_wg_per_cu(int rf_decim) { return rf_decim == 9 ? 8 : kVariants[variant_index()].wg_per_cu; }
+
 int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_decim,
                       int audio_down, const MonoTaps& taps, hipStream_t s) {
-#define FMRX_VARIANT(T_, D_, AD_)                                                  \
-    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_)                      \
-        return launch_variant<T_, D_, AD_, kNT, kR>(L, n_streams, taps, s);
-    FMRX_VARIANT(51, 10, 5)    // mode 0, reference taps
-    FMRX_VARIANT(101, 10, 5)   // mode 0, 101-tap RF (BASELINE config 2)
-    FMRX_VARIANT(51, 4, 6)     // mode 1
-    FMRX_VARIANT(101, 4, 6)
-#undef FMRX_VARIANT
+    const int vi = variant_index();
+#define FMRX_V(T_, D_, AD_, I_, NT_, R_, PD_)                                              \
+    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == I_)                  \
+        return launch_variant<T_, D_, AD_, NT_, R_, PD_>(L, n_streams, taps, s);
+#define FMRX_ALL(T_, D_, AD_)           \
+    FMRX_V(T_, D_, AD_, 0, 256, 3, 3)   \
+    FMRX_V(T_, D_, AD_, 1, 128, 3, 3)   \
+    FMRX_V(T_, D_, AD_, 2, 64, 3, 3)    \
+    FMRX_V(T_, D_, AD_, 3, 128, 5, 3)   \
+    FMRX_V(T_, D_, AD_, 4, 256, 3, 5)
+    FMRX_ALL(51, 10, 5)    // mode 0 (and mode 2's RF stage), reference taps
+    FMRX_ALL(101, 10, 5)   // mode 0, 101-tap RF (BASELINE configs[1])
+    FMRX_ALL(51, 4, 6)     // mode 1
+    FMRX_ALL(101, 4, 6)
+    // mode 3 (odd decimation 9): R = 2 keeps the per-thread stride S = 18 even; the
+    // polyphase 441/2560 audio stage runs separately, so AD is a placeholder here
+    if (rf_decim == 9 && rf_taps == 51) return launch_variant<51, 9, 5, 64, 2, 3>(L, n_streams, taps, s);
+    if (rf_decim == 9 && rf_taps == 101) return launch_variant<101, 9, 5, 64, 2, 3>(L, n_streams, taps, s);
+#undef FMRX_ALL
+#undef FMRX_V
     return -1;
 }
 

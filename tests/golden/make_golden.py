@@ -49,6 +49,7 @@ CASES = [
     ("m1_rf51_synth", 1, 51, "synth:4", 12, ALL),
     ("m1_rf101_rand", 1, 101, "rand:9", 6, ["demod", "mono_indep", "pcm", "pcm_mono"]),
     ("m2_rf51_synth", 2, 51, "synth:5", 2, ["pcm", "pcm_mono", "pll_state"]),
+    ("m3_rf51_synth", 3, 51, "synth:6", 1, ["pcm", "pcm_mono", "pll_state"]),
 ]
 # Long runs, hash only: (name, mode, rf_taps, recipe, seconds of signal)
 LONG = [
@@ -56,6 +57,8 @@ LONG = [
     ("m0_rf101_synth_10s", 0, 101, "synth:12", 10.0),
     ("m1_rf51_synth_10s", 1, 51, "synth:13", 10.0),
     ("m2_rf51_synth_4s", 2, 51, "synth:14", 4.0),
+    ("m3_rf51_synth_8s", 3, 51, "synth:15", 8.0),
+    ("m0_rf51_rand_2s", 0, 51, "rand:16", 2.0),
 ]
 
 

@@ -223,10 +223,12 @@ def test_stereo_long_hash(fmrx, name):
         assert sha(rx.process(iq)) == h["pcm_sha256"]
 
 
-def test_mode2_mono_long_hash(fmrx):
-    h = long_runs()["m2_rf51_synth_4s"]
-    iq = iqgen.make(h["recipe"], h["n_blocks"] * 2048000, 2400000)
-    with fmrx.Receiver(2, fmrx.MONO) as rx:
+@pytest.mark.parametrize("name", [n for n in long_runs() if long_runs()[n]["mode"] in (2, 3)])
+def test_polyphase_mono_long_hash(fmrx, name):
+    h = long_runs()[name]
+    bb, rf_fs = oracle.MODES[h["mode"]][0], oracle.MODES[h["mode"]][3]
+    iq = iqgen.make(h["recipe"], h["n_blocks"] * bb, rf_fs)
+    with fmrx.Receiver(h["mode"], fmrx.MONO, rf_taps=h["rf_taps"]) as rx:
         assert sha(rx.process(iq)) == h["pcm_mono_sha256"]
 
 
