@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -70,6 +71,7 @@ struct DevBuf {
 }  // namespace
 
 struct fmrx_ctx {
+    mutable std::recursive_mutex mu;  // every entry point holds it: one call on a context at a time
     fmrx_config cfg{};
     fmrx_geometry_t geo{};
     ModeConstants mc{};
@@ -106,6 +108,23 @@ struct fmrx_ctx {
 };
 
 namespace {
+
+// Serialises the entry points of one context (rf and audio stages may be driven from two
+// threads, as project.cpp does; they share the context's stream and scratch buffers).
+class CtxLock {
+  public:
+    explicit CtxLock(const fmrx_ctx* c) : c_(c) {
+        if (c_) c_->mu.lock();
+    }
+    ~CtxLock() {
+        if (c_) c_->mu.unlock();
+    }
+    CtxLock(const CtxLock&) = delete;
+    CtxLock& operator=(const CtxLock&) = delete;
+
+  private:
+    const fmrx_ctx* c_;
+};
 
 bool fused_rf_supported(const fmrx_ctx* c) {
     const int t = c->geo.rf_taps, d = c->geo.rf_decim;
@@ -412,6 +431,7 @@ void fmrx_destroy(fmrx_ctx* c) {
 }
 
 int fmrx_reset(fmrx_ctx* c) {
+    CtxLock lock_(c);
     if (!c) return fail(FMRX_EINVAL, "null context");
     int rc = set_device(c);
     return rc ? rc : reset_state(c);
@@ -419,6 +439,7 @@ int fmrx_reset(fmrx_ctx* c) {
 
 // ---- state blob: header + halo bytes + audio history + stereo state ------------------
 int fmrx_state_size(const fmrx_ctx* c, size_t* bytes) {
+    CtxLock lock_(c);
     if (!c || !bytes) return fail(FMRX_EINVAL, "null argument");
     const size_t ns = c->cfg.n_streams;
     *bytes = 8 * sizeof(uint32_t) + ns * (c->halo_bytes + sizeof(float) * (c->audio_hist + kDemodHist + 8 + kMixTail + 8));
@@ -469,11 +490,13 @@ int state_io(fmrx_ctx* c, uint8_t* buf, size_t bytes, bool put) {
 }  // namespace
 
 int fmrx_get_state(fmrx_ctx* c, void* buf, size_t bytes) {
+    CtxLock lock_(c);
     if (!c || !buf) return fail(FMRX_EINVAL, "null argument");
     return state_io(c, static_cast<uint8_t*>(buf), bytes, false);
 }
 
 int fmrx_set_state(fmrx_ctx* c, const void* buf, size_t bytes) {
+    CtxLock lock_(c);
     if (!c || !buf) return fail(FMRX_EINVAL, "null argument");
     return state_io(c, static_cast<uint8_t*>(const_cast<void*>(buf)), bytes, true);
 }
@@ -481,6 +504,7 @@ int fmrx_set_state(fmrx_ctx* c, const void* buf, size_t bytes) {
 // ---- fused device-resident path ----------------------------------------------------------
 int fmrx_process_device_ex(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
                            float* d_mono) {
+    CtxLock lock_(c);
     if (!c || !d_iq || !d_pcm) return fail(FMRX_EINVAL, "null argument");
     if (n_blocks == 0) return FMRX_OK;
     int rc = set_device(c);
@@ -506,6 +530,7 @@ int fmrx_process_device(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16
 }
 
 int fmrx_synchronize(fmrx_ctx* c) {
+    CtxLock lock_(c);
     if (!c) return fail(FMRX_EINVAL, "null context");
     HIPCHK(hipStreamSynchronize(c->stream));
     return FMRX_OK;
@@ -514,6 +539,7 @@ int fmrx_synchronize(fmrx_ctx* c) {
 void* fmrx_stream(fmrx_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int fmrx_kernel_timing(fmrx_ctx* c, int reset, double* avg_ms, long* launches) {
+    CtxLock lock_(c);
     if (!c) return fail(FMRX_EINVAL, "null context");
     int rc = set_device(c);
     if (rc) return rc;
@@ -538,6 +564,7 @@ int fmrx_kernel_timing(fmrx_ctx* c, int reset, double* avg_ms, long* launches) {
 
 // ---- host-buffer entry points ---------------------------------------------------------------
 int fmrx_process(fmrx_ctx* c, const uint8_t* iq, size_t n_blocks, int16_t* pcm) {
+    CtxLock lock_(c);
     if (!c || !iq || !pcm) return fail(FMRX_EINVAL, "null argument");
     if (n_blocks == 0) return FMRX_OK;
     int rc = set_device(c);
@@ -555,6 +582,7 @@ int fmrx_process(fmrx_ctx* c, const uint8_t* iq, size_t n_blocks, int16_t* pcm) 
 
 // rf_thread body (project.cpp:48-70): u8 blocks -> demod floats.
 int fmrx_rf_block(fmrx_ctx* c, const uint8_t* iq, size_t n_blocks, float* demod) {
+    CtxLock lock_(c);
     if (!c || !iq || !demod) return fail(FMRX_EINVAL, "null argument");
     if (n_blocks == 0) return FMRX_OK;
     int rc = set_device(c);
@@ -572,6 +600,7 @@ int fmrx_rf_block(fmrx_ctx* c, const uint8_t* iq, size_t n_blocks, float* demod)
 
 // audio_thread body (project.cpp:132-195): demod floats -> S16.
 int fmrx_audio_block(fmrx_ctx* c, const float* demod, size_t n_blocks, int16_t* pcm) {
+    CtxLock lock_(c);
     if (!c || !demod || !pcm) return fail(FMRX_EINVAL, "null argument");
     if (n_blocks == 0) return FMRX_OK;
     int rc = set_device(c);
@@ -611,6 +640,7 @@ int fmrx_impulse_response_bpf(float* h, float fs, float fb, float fe, int taps) 
 
 int fmrx_resample(fmrx_ctx* c, float* d_out, float* d_state, const float* d_in, int n_in,
                   const float* d_coeff, int taps, int up, int down, int* n_out) {
+    CtxLock lock_(c);
     if (!c || !d_out || !d_state || !d_in || !d_coeff || taps < 1 || up < 1 || down < 1)
         return fail(FMRX_EINVAL, "bad argument");
     if (n_in < taps - 1) return fail(FMRX_EINVAL, "input shorter than the filter history");
@@ -625,6 +655,7 @@ int fmrx_resample(fmrx_ctx* c, float* d_out, float* d_state, const float* d_in, 
 }
 
 int fmrx_fm_demod(fmrx_ctx* c, float* d_out, float* d_prev, const float* d_i, const float* d_q, int n) {
+    CtxLock lock_(c);
     if (!c || !d_out || !d_prev || !d_i || !d_q || n < 0) return fail(FMRX_EINVAL, "bad argument");
     int rc = set_device(c);
     if (rc) return rc;
@@ -633,6 +664,7 @@ int fmrx_fm_demod(fmrx_ctx* c, float* d_out, float* d_prev, const float* d_i, co
 
 int fmrx_pll(fmrx_ctx* c, float* d_io, int n, float freq, float fs, float nco_scale, float phase_adjust,
              float norm_bw, float* d_st) {
+    CtxLock lock_(c);
     if (!c || !d_io || !d_st || n < 0) return fail(FMRX_EINVAL, "bad argument");
     int rc = set_device(c);
     if (rc) return rc;
@@ -647,6 +679,7 @@ int fmrx_pll(fmrx_ctx* c, float* d_io, int n, float freq, float fs, float nco_sc
 }
 
 int fmrx_mixer(fmrx_ctx* c, float* d_out, const float* d_a, const float* d_b, int n) {
+    CtxLock lock_(c);
     if (!c || !d_out || !d_a || !d_b || n < 0) return fail(FMRX_EINVAL, "bad argument");
     int rc = set_device(c);
     if (rc) return rc;
@@ -654,6 +687,7 @@ int fmrx_mixer(fmrx_ctx* c, float* d_out, const float* d_a, const float* d_b, in
 }
 
 int fmrx_lr_extraction(fmrx_ctx* c, float* d_l, float* d_r, const float* d_m, const float* d_s, int n) {
+    CtxLock lock_(c);
     if (!c || !d_l || !d_r || !d_m || !d_s || n < 0) return fail(FMRX_EINVAL, "bad argument");
     int rc = set_device(c);
     if (rc) return rc;
@@ -661,6 +695,7 @@ int fmrx_lr_extraction(fmrx_ctx* c, float* d_l, float* d_r, const float* d_m, co
 }
 
 int fmrx_normalize_iq(fmrx_ctx* c, const uint8_t* d_iq, size_t n_pairs, float* d_i, float* d_q) {
+    CtxLock lock_(c);
     if (!c || !d_iq || !d_i || !d_q) return fail(FMRX_EINVAL, "bad argument");
     int rc = set_device(c);
     if (rc) return rc;
@@ -668,6 +703,7 @@ int fmrx_normalize_iq(fmrx_ctx* c, const uint8_t* d_iq, size_t n_pairs, float* d
 }
 
 int fmrx_quantize(fmrx_ctx* c, const float* d_x, size_t n, int16_t* d_out) {
+    CtxLock lock_(c);
     if (!c || !d_x || !d_out) return fail(FMRX_EINVAL, "bad argument");
     int rc = set_device(c);
     if (rc) return rc;
@@ -686,6 +722,7 @@ int fmrx_synth_host(uint64_t seed, int rf_fs, uint64_t first_pair, size_t n_pair
 
 int fmrx_synth_device(fmrx_ctx* c, uint64_t seed, int rf_fs, uint64_t first_pair, size_t n_pairs,
                       uint8_t* d_out) {
+    CtxLock lock_(c);
     if (!c || !d_out || rf_fs <= 0) return fail(FMRX_EINVAL, "bad argument");
     int rc = set_device(c);
     if (rc) return rc;
