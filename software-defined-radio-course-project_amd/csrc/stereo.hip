@@ -12,6 +12,7 @@
 
 #include "dsp_device.h"
 #include "fmrx_internal.h"
+#include "pll_math.h"
 
 namespace fmrx {
 
@@ -62,10 +63,45 @@ __global__ void bpf_pair_generic(StereoLaunch L, BpTaps t) {
 }
 
 // src/filter.cpp:136-174 PLL.  A nonlinear recurrence: strictly serial in time, so one lane
-// per stream.  Float state, double-precision atan2 / cos / sin as the reference's libm calls;
+// per stream.  Float state; the reference's double atan2 / cos / sin results rounded to
+// float come from pll_math.h's certified fast path (fallback: the full library call).
 // st = {integrator, phaseEst, feedbackI, feedbackQ, ncoOut_state, trigOffset} (stride 8).
+//
+// The recurrence only needs atan2 and sincos; the NCO output cos(trigArg * ncoScale +
+// phaseAdjust) (filter.cpp:170) depends on nothing later, so the serial loop stores trigArg
+// in place and pll_nco_kernel evaluates the NCO for all samples in parallel afterwards.
+__device__ __noinline__ float atan2_lib(float y, float x) {
+    return static_cast<float>(atan2(static_cast<double>(y), static_cast<double>(x)));
+}
+__device__ __noinline__ void sincos_lib(float a, float* s, float* c) {
+    *s = static_cast<float>(sin(static_cast<double>(a)));
+    *c = static_cast<float>(cos(static_cast<double>(a)));
+}
+
+struct PllState {
+    float integ, phase, fbI, fbQ, trig;
+};
+
+__device__ inline float pll_step(PllState& p, float v, float Ki, float Kp, double step) {
+    const float eI = v * p.fbI;
+    const float eQ = v * (-p.fbQ);
+    float e;
+    if (!fast_atan2_f(eQ, eI, &e)) e = atan2_lib(eQ, eI);
+    p.integ = p.integ + Ki * e;
+    p.phase = p.phase + ((Kp * e) + p.integ);
+    p.trig = p.trig + 1.0f;
+    const float arg = static_cast<float>(step * static_cast<double>(p.trig) + static_cast<double>(p.phase));
+    float sv, cv;
+    if (!fast_sincos_f(arg, &sv, &cv)) sincos_lib(arg, &sv, &cv);
+    p.fbI = cv;
+    p.fbQ = sv;
+    return arg;
+}
+
+constexpr int kPllBatch = 16;  // samples prefetched per batch (4 x 16-B loads)
+
 __global__ void pll_kernel(float* io, int n, int n_streams, size_t stride, float freq, float fs,
-                           float nco_scale, float phase_adjust, float norm_bw, float* st) {
+                           float norm_bw, float* st) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_streams) return;
     float* x = io + (size_t)s * stride;
@@ -74,23 +110,49 @@ __global__ void pll_kernel(float* io, int n, int n_streams, size_t stride, float
     const float Ci = static_cast<float>(3.555);
     const float Kp = norm_bw * Cp;
     const float Ki = (norm_bw * norm_bw) * Ci;
-    float integ = S[0], phase = S[1], fbI = S[2], fbQ = S[3], trig = S[5];
+    PllState p{S[0], S[1], S[2], S[3], S[5]};
     const double step = (2.0 * kPi) * static_cast<double>(freq / fs);
-    for (int i = 0; i < n; i++) {
-        const float v = x[i];
-        const float eI = v * fbI;
-        const float eQ = v * (-fbQ);
-        const float e = static_cast<float>(atan2(static_cast<double>(eQ), static_cast<double>(eI)));
-        integ = integ + Ki * e;
-        phase = phase + ((Kp * e) + integ);
-        trig = trig + 1.0f;
-        const float arg = static_cast<float>(step * static_cast<double>(trig) + static_cast<double>(phase));
-        fbI = static_cast<float>(cos(static_cast<double>(arg)));
-        fbQ = static_cast<float>(sin(static_cast<double>(arg)));
-        x[i] = static_cast<float>(cos(static_cast<double>(arg * nco_scale + phase_adjust)));
+    int i = 0;
+    if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+        // batches of 16 with the next batch in flight while this one runs
+        float4 cur[4], nxt[4];
+        const int nb = n / kPllBatch;
+        if (nb > 0)
+            for (int q = 0; q < 4; q++) cur[q] = reinterpret_cast<const float4*>(x)[q];
+        for (int b = 0; b < nb; b++) {
+            if (b + 1 < nb)
+                for (int q = 0; q < 4; q++)
+                    nxt[q] = reinterpret_cast<const float4*>(x + (b + 1) * kPllBatch)[q];
+            float4 out[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                out[q].x = pll_step(p, cur[q].x, Ki, Kp, step);
+                out[q].y = pll_step(p, cur[q].y, Ki, Kp, step);
+                out[q].z = pll_step(p, cur[q].z, Ki, Kp, step);
+                out[q].w = pll_step(p, cur[q].w, Ki, Kp, step);
+            }
+            for (int q = 0; q < 4; q++) reinterpret_cast<float4*>(x + b * kPllBatch)[q] = out[q];
+            for (int q = 0; q < 4; q++) cur[q] = nxt[q];
+        }
+        i = nb * kPllBatch;
     }
-    S[0] = integ; S[1] = phase; S[2] = fbI; S[3] = fbQ; S[5] = trig;
-    if (n > 0) S[4] = x[n - 1];
+    for (; i < n; i++) x[i] = pll_step(p, x[i], Ki, Kp, step);
+    S[0] = p.integ; S[1] = p.phase; S[2] = p.fbI; S[3] = p.fbQ; S[5] = p.trig;
+}
+
+// filter.cpp:170: ncoOut[i] = cos(trigArg * nocoScale + phaseAdjust), float arithmetic inside,
+// double cos, float result; also the ncoOut_state carry (filter.cpp:173).
+__global__ void pll_nco_kernel(float* io, int n, size_t stride, float nco_scale, float phase_adjust,
+                               float* st) {
+    const int s = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float* x = io + (size_t)s * stride;
+    const float a = x[i] * nco_scale + phase_adjust;
+    float sv, cv;
+    if (!fast_sincos_f(a, &sv, &cv)) cv = static_cast<float>(cos(static_cast<double>(a)));
+    x[i] = cv;
+    if (i == n - 1) st[8 * (size_t)s + 4] = cv;
 }
 
 // ---- audio stage -------------------------------------------------------------------------
@@ -211,7 +273,9 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
                float nco_scale, float phase_adjust, float norm_bw, float* st, hipStream_t s) {
     if (n <= 0) return 0;
     hipLaunchKernelGGL(pll_kernel, dim3((n_streams + 63) / 64), dim3(64), 0, s, io, n, n_streams,
-                       stride, freq, fs, nco_scale, phase_adjust, norm_bw, st);
+                       stride, freq, fs, norm_bw, st);
+    hipLaunchKernelGGL(pll_nco_kernel, dim3((n + 255) / 256, n_streams), dim3(256), 0, s, io, n,
+                       stride, nco_scale, phase_adjust, st);
     return ok();
 }
 

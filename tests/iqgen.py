@@ -17,12 +17,22 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "software-defined-radio-course-project_amd")
 
 
+_MODS = {}
+
+
+def load_module(name: str):
+    """Import a module of the product package (its dir name is not a Python identifier)."""
+    if name not in _MODS:
+        spec = importlib.util.spec_from_file_location(name, os.path.join(PKG, name + ".py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _MODS[name] = mod
+    return _MODS[name]
+
+
 def load_fmrx():
-    """Import the product binding (package dir name is not a Python identifier)."""
-    spec = importlib.util.spec_from_file_location("fmrx", os.path.join(PKG, "fmrx.py"))
-    mod = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(mod)
-    return mod
+    """Import the product binding, software-defined-radio-course-project_amd/fmrx.py."""
+    return load_module("fmrx")
 
 
 def splitmix64(x: np.ndarray) -> np.ndarray:

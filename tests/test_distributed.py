@@ -1,0 +1,52 @@
+"""Multi-process sharding + gather (BASELINE configs[4]) on CPU: world_size 2, gloo.
+
+The per-rank work is the oracle (CPU) instead of libfmrx (GPU); the sharding, padding and
+gather code is the same code path the GPU runner uses over RCCL."""
+from __future__ import annotations
+
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import iqgen
+import oracle
+
+MODE, NB, BB, NA = 0, 2, 12800, 128
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shard_balanced_and_covering():
+    d = iqgen.load_module("dist")
+    for n in (1, 5, 8, 31, 256):
+        for w in (1, 2, 3, 8):
+            rs = [d.shard(n, w, r) for r in range(w)]
+            assert [i for r in rs for i in r] == list(range(n))
+            assert max(map(len, rs)) - min(map(len, rs)) <= 1
+
+
+@pytest.mark.parametrize("n_streams", [5, 2, 1])
+def test_gather_world2_matches_serial(n_streams, orc, tmp_path):
+    port = _free_port()
+    out = tmp_path / "pcm.npy"
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
+                   WORLD_SIZE="2", LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"),
+                                       str(n_streams), str(out)], env=env))
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    got = np.load(out)
+    want = np.stack([orc.run(MODE, 51, iqgen.make(f"rand:{100 + i}", NB * BB), ["pcm"])["pcm"]
+                     for i in range(n_streams)])
+    assert got.shape == want.shape and np.array_equal(got, want)
