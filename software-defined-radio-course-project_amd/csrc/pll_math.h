@@ -126,4 +126,106 @@ FMRX_HD bool fast_atan2_f(float yf, float xf, float* out) {
     return decide_float(a, 3.0e-15 * fabs(a), out);
 }
 
+// ---- the PLL step (src/filter.cpp:157-171) with a short dependency chain ----------------
+//
+// The phase error e = atan2(eQ, eI) with (eI, eQ) = v * (fbI, -fbQ), fbI/fbQ = float(cos/sin
+// of the previous trigArg phi).  The previous step's sincos left cos(phi), sin(phi) in DOUBLE
+// (C, S) and phi's reduction phi = r + q*pi/2 (mod 2 pi).  Rotating (eI, eQ) by +phi gives
+// (X, Y) with angle theta + phi = a tiny residual d (float roundings only, |d| < 1e-6) or
+// pi + d when v < 0, hence  theta = atan(Y/X) + [X<0] pi - r - q pi/2  (mod 2 pi),  with
+// atan(Y/X) = Y/X to 1e-18 at that size.  Absolute error budget: (C, S) angle 1.5e-15,
+// rotation 3e-16, r 1e-16, constants 2e-16, glibc 1 ulp(pi) 4.4e-16 -> E = 4e-15, certified
+// by decide_float like the kernels above; anything else takes the generic path.
+
+struct PllCtx {
+    double C, S, r;  // cos/sin(phi) and phi's reduced argument from the last sincos
+    int q;           // phi's quadrant, phi = r + q*pi/2 (mod 2 pi)
+    bool valid;
+};
+
+constexpr double kPiHi = 3.14159265358979311600e+00;
+
+FMRX_HD bool rot_atan2_f(float eQ, float eI, const PllCtx& c, float* out) {
+    // Branch-free: every test folds into one predicate (the PLL runs one lane per stream,
+    // where each taken-or-not branch costs as much as several arithmetic ops).
+    const double ei = (double)eI, eq = (double)eQ;
+    const double X = fma(ei, c.C, -(eq * c.S));
+    const double Y = fma(ei, c.S, eq * c.C);
+    // 1/X: hardware reciprocal estimate + one Newton step (relative error ~2^-52; |d| < 1e-4
+    // makes its contribution < 1e-20 absolute)
+#ifdef __HIP_DEVICE_COMPILE__
+    const double y0 = __builtin_amdgcn_rcp(X);
+#else
+    const double y0 = 1.0 / X;
+#endif
+    const double y1 = fma(y0, fma(-X, y0, 1.0), y0);
+    const double d = Y * y1;
+    const int k = ((X < 0.0 ? 2 : 0) - c.q) & 3;
+    const double kd = (double)k;
+    const double t0 = fma(kd, kPio2Lo, fma(kd, kPio2Hi, d - c.r));
+    const double th = t0 > kPiHi ? (t0 - 2.0 * kPiHi) - 2.0 * kPiLo : t0;
+    const float lo = (float)(th - 4.0e-15), hi = (float)(th + 4.0e-15);
+    *out = (float)th;
+    // zeros (C99 signed-zero rules), residual too large, too close to the +-pi cut, or an
+    // uncertified rounding: generic path
+    return (int)c.valid & (int)(eI != 0.0f) & (int)(eQ != 0.0f) & (int)(fabs(d) < 1.0e-4) &
+           (int)(fabs(fabs(th) - kPiHi) > 1.0e-9) & (int)(lo == hi);
+}
+
+// sin/cos of a float argument with the context for the next rot_atan2_f.
+FMRX_HD bool sincos_ctx_f(float xf, float* s_out, float* c_out, PllCtx* ctx) {
+    const double x = (double)xf;
+    const bool in_range = (int)(fabs(x) < 1.0e9) & (int)(fabs(x) > 1.0e-30);  // rejects inf/nan/0
+    const double nd = rint(in_range ? x * kInvPio2 : 0.0);
+    const double r1 = fma(-nd, kPio2Hi, x);
+    const double r = fma(-nd, kPio2Lo, r1);
+    const double z = r * r, z2 = z * z, z4 = z2 * z2;
+    // same fdlibm kernels in Estrin form (shorter dependency chain)
+    const double ps = fma(z4, fma(z, kS6, kS5), fma(z2, fma(z, kS4, kS3), fma(z, kS2, kS1)));
+    const double sn = fma(z * r, ps, r);
+    const double pc = fma(z4, fma(z, kC6, kC5), fma(z2, fma(z, kC4, kC3), fma(z, kC2, kC1)));
+    const double cs = 1.0 - (0.5 * z - (z * z) * pc);
+    const int q = (int)((long long)nd & 3);
+    const double sv = (q & 1) ? cs : sn, cv0 = (q & 1) ? sn : cs;
+    const double s2 = (q & 2) ? -sv : sv;
+    const double c2 = ((q + 1) & 2) ? -cv0 : cv0;
+    const double ea = fabs(nd) * 1.0e-32;
+    const bool s_ok = decide_float(s2, 1.5e-15 * fabs(s2) + ea, s_out);
+    const bool c_ok = decide_float(c2, 1.5e-15 * fabs(c2) + ea, c_out);
+    // (C, S, r, q) are within the bounds rot_atan2_f assumes whether or not the float
+    // rounding could be certified here, so the context is valid either way.
+    ctx->C = c2;
+    ctx->S = s2;
+    ctx->r = r;
+    ctx->q = q;
+    ctx->valid = in_range;
+    return (int)in_range & (int)s_ok & (int)c_ok;
+}
+
+struct PllState {
+    float integ, phase, fbI, fbQ, trig;
+};
+
+// One PLL iteration; returns trigArg (the NCO is cos(trigArg * ncoScale + phaseAdjust)).
+// Lib supplies the out-of-line paths: atan2f_(y, x) (fast_atan2_f, then the library) and
+// sincosf_(a, &s, &c) (the library).
+template <class Lib>
+FMRX_HD float pll_step(PllState& p, PllCtx& ctx, float v, float Ki, float Kp, double step,
+                       const Lib& lib) {
+    const float eI = v * p.fbI;
+    const float eQ = v * (-p.fbQ);
+    float e;
+    if (!rot_atan2_f(eQ, eI, ctx, &e)) e = lib.atan2f_(eQ, eI);  // generic certified path
+    p.integ = p.integ + Ki * e;
+    p.phase = p.phase + ((Kp * e) + p.integ);
+    p.trig = p.trig + 1.0f;
+    const double prod = step * (double)p.trig;
+    const float arg = (float)(prod + (double)p.phase);
+    float sv, cv;
+    if (!sincos_ctx_f(arg, &sv, &cv, &ctx)) lib.sincosf_(arg, &sv, &cv);
+    p.fbI = cv;
+    p.fbQ = sv;
+    return arg;
+}
+
 }  // namespace fmrx

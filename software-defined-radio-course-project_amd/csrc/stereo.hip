@@ -70,33 +70,25 @@ __global__ void bpf_pair_generic(StereoLaunch L, BpTaps t) {
 // The recurrence only needs atan2 and sincos; the NCO output cos(trigArg * ncoScale +
 // phaseAdjust) (filter.cpp:170) depends on nothing later, so the serial loop stores trigArg
 // in place and pll_nco_kernel evaluates the NCO for all samples in parallel afterwards.
+// Full-precision fallbacks (HIP's double atan2/sin/cos), out of line: taken ~1e-7 of calls.
 __device__ __noinline__ float atan2_lib(float y, float x) {
+    float e;
+    if (fast_atan2_f(y, x, &e)) return e;
     return static_cast<float>(atan2(static_cast<double>(y), static_cast<double>(x)));
 }
-__device__ __noinline__ void sincos_lib(float a, float* s, float* c) {
-    *s = static_cast<float>(sin(static_cast<double>(a)));
-    *c = static_cast<float>(cos(static_cast<double>(a)));
+__device__ __noinline__ float2 sincos_lib(float a) {
+    return make_float2(static_cast<float>(sin(static_cast<double>(a))),
+                       static_cast<float>(cos(static_cast<double>(a))));
 }
 
-struct PllState {
-    float integ, phase, fbI, fbQ, trig;
+struct DeviceLib {
+    __device__ float atan2f_(float y, float x) const { return atan2_lib(y, x); }
+    __device__ void sincosf_(float a, float* s, float* c) const {
+        const float2 r = sincos_lib(a);
+        *s = r.x;
+        *c = r.y;
+    }
 };
-
-__device__ inline float pll_step(PllState& p, float v, float Ki, float Kp, double step) {
-    const float eI = v * p.fbI;
-    const float eQ = v * (-p.fbQ);
-    float e;
-    if (!fast_atan2_f(eQ, eI, &e)) e = atan2_lib(eQ, eI);
-    p.integ = p.integ + Ki * e;
-    p.phase = p.phase + ((Kp * e) + p.integ);
-    p.trig = p.trig + 1.0f;
-    const float arg = static_cast<float>(step * static_cast<double>(p.trig) + static_cast<double>(p.phase));
-    float sv, cv;
-    if (!fast_sincos_f(arg, &sv, &cv)) sincos_lib(arg, &sv, &cv);
-    p.fbI = cv;
-    p.fbQ = sv;
-    return arg;
-}
 
 constexpr int kPllBatch = 16;  // samples prefetched per batch (4 x 16-B loads)
 
@@ -111,6 +103,9 @@ __global__ void pll_kernel(float* io, int n, int n_streams, size_t stride, float
     const float Kp = norm_bw * Cp;
     const float Ki = (norm_bw * norm_bw) * Ci;
     PllState p{S[0], S[1], S[2], S[3], S[5]};
+    PllCtx ctx{};
+    ctx.valid = false;
+    const DeviceLib lib;
     const double step = (2.0 * kPi) * static_cast<double>(freq / fs);
     int i = 0;
     if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
@@ -126,17 +121,17 @@ __global__ void pll_kernel(float* io, int n, int n_streams, size_t stride, float
             float4 out[4];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                out[q].x = pll_step(p, cur[q].x, Ki, Kp, step);
-                out[q].y = pll_step(p, cur[q].y, Ki, Kp, step);
-                out[q].z = pll_step(p, cur[q].z, Ki, Kp, step);
-                out[q].w = pll_step(p, cur[q].w, Ki, Kp, step);
+                out[q].x = pll_step(p, ctx, cur[q].x, Ki, Kp, step, lib);
+                out[q].y = pll_step(p, ctx, cur[q].y, Ki, Kp, step, lib);
+                out[q].z = pll_step(p, ctx, cur[q].z, Ki, Kp, step, lib);
+                out[q].w = pll_step(p, ctx, cur[q].w, Ki, Kp, step, lib);
             }
             for (int q = 0; q < 4; q++) reinterpret_cast<float4*>(x + b * kPllBatch)[q] = out[q];
             for (int q = 0; q < 4; q++) cur[q] = nxt[q];
         }
         i = nb * kPllBatch;
     }
-    for (; i < n; i++) x[i] = pll_step(p, x[i], Ki, Kp, step);
+    for (; i < n; i++) x[i] = pll_step(p, ctx, x[i], Ki, Kp, step, lib);
     S[0] = p.integ; S[1] = p.phase; S[2] = p.fbI; S[3] = p.fbQ; S[5] = p.trig;
 }
 

@@ -59,6 +59,7 @@ LONG = [
     ("m2_rf51_synth_4s", 2, 51, "synth:14", 4.0),
     ("m3_rf51_synth_8s", 3, 51, "synth:15", 8.0),
     ("m0_rf51_rand_2s", 0, 51, "rand:16", 2.0),
+    ("m0_rf51_synth_72s", 0, 51, "synth:17", 72.0),  # PLL trigOffset saturates at 69.9 s
 ]
 
 

@@ -32,3 +32,31 @@ def test_atan2_fast_path_matches_glibc(checker):
     r = subprocess.run([checker, "atan2", "20000000", "3"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout
     assert "mismatches=0" in r.stdout
+
+
+@pytest.fixture(scope="module")
+def runner(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("pllr") / "check_pll_run")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", exe,
+                    os.path.join(REPO, "tools", "check_pll_run.cpp")], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("recipe,seconds,chunk", [("synth:5", 12.0, 640), ("rand:6", 3.0, 6400),
+                                                  ("const128", 0.5, 640), ("synth:8", 72.0, 1 << 30)])
+def test_pll_recurrence_bit_exact(runner, orc, tmp_path, recipe, seconds, chunk):
+    """The whole PLL recurrence with the GPU's step function (rotation atan2 + certified
+    sincos + fallbacks) equals the reference arithmetic bit for bit; the 72 s run crosses
+    the float trigOffset saturation at 2^24 samples (69.9 s)."""
+    import numpy as np
+
+    import iqgen
+
+    nb = int(seconds * 2400000 * 2 // 12800)
+    iq = iqgen.make(recipe, nb * 12800)
+    carrier = orc.run(0, 51, iq, ["carrier"])["carrier"]
+    f = tmp_path / "carrier.f32"
+    carrier.astype(np.float32).tofile(f)
+    r = subprocess.run([runner, str(f), "19000", "240000", str(chunk)], capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0 and "mismatches=0 state_equal=1" in r.stdout, r.stdout
