@@ -94,7 +94,9 @@ __device__ inline float sbyte(uint32_t w) {
     return f;
 }
 
-template <int T, int D, int AD, int NT, int R, int PD>
+// ABL (timing ablations only, never selected in production): bit 1 skips the RF FIR, 2 the
+// audio FIR, 4 the demod, 8 the byte conversion of the staging.
+template <int T, int D, int AD, int NT, int R, int PD, int ABL = 0, int PF = 1>
 __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps taps) {
     using C = MonoCfg<T, D, AD, NT, R>;
     constexpr int CIF = C::CIF, P = C::P, H = C::H, S = C::S, G = C::G, NLD = C::NLD;
@@ -131,11 +133,27 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         const uint32_t w = load4(in, halo, ((c0 - 1) * (long long)P - H + 2 * i) * 2, total, hb) ^ 0x80808080u;
         xb4[C::slot(2 * i) / 2] = make_float4(sbyte<0>(w), sbyte<1>(w), sbyte<2>(w), sbyte<3>(w));
     }
-    uint32_t pf[NLD];
+    // Input prefetch, PF chunks ahead: pf holds chunk c, pf2 (PF == 2) chunk c+1.
+    uint32_t pf[NLD], pf2[NLD];
+    auto fetch = [&](long long cc, uint32_t (&dst)[NLD]) {
+        const long long nb0 = cc * 2LL * P;  // first byte of chunk cc
+        if (nb0 >= 0 && nb0 + 2LL * P <= total) {
+            // interior chunk (all but the ends of a stream): plain coalesced dword loads
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(in + nb0) + tid;
 #pragma unroll
-    for (int l = 0; l < NLD; l++) {
-        const int u = tid + l * NT;
-        if (u < P / 2) pf[l] = load4(in, halo, (c0 - 1) * 2LL * P + 4LL * u, total, hb);
+            for (int l = 0; l < NLD; l++)
+                if ((P / 2) % NT == 0 || tid + l * NT < P / 2) dst[l] = src[l * NT];
+        } else {
+#pragma unroll
+            for (int l = 0; l < NLD; l++) {
+                const int u = tid + l * NT;
+                if (u < P / 2) dst[l] = load4(in, halo, nb0 + 4LL * u, total, hb);
+            }
+        }
+    };
+    fetch(c0 - 1, pf);
+    if constexpr (PF == 2) {
+        if (c0 < c1) fetch(c0, pf2);
     }
 
     int cur = 0;
@@ -147,25 +165,19 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
             const int u = tid + l * NT;
             if ((P / 2) % NT == 0 || u < P / 2) {
                 const uint32_t w = pf[l] ^ 0x80808080u;
-                xb4[C::slot(H + 2 * u) / 2] = make_float4(sbyte<0>(w), sbyte<1>(w), sbyte<2>(w), sbyte<3>(w));
+                if constexpr ((ABL & 8) != 0)
+                    xb4[C::slot(H + 2 * u) / 2] = make_float4(__uint_as_float(w), 0.f, 0.f, 0.f);
+                else
+                    xb4[C::slot(H + 2 * u) / 2] = make_float4(sbyte<0>(w), sbyte<1>(w), sbyte<2>(w), sbyte<3>(w));
             }
         }
         __syncthreads();  // (A) chunk c staged, carry from c-1 in place
-        if (c + 1 < c1) {
-            const long long nb0 = (c + 1) * 2LL * P;  // first byte of chunk c+1
-            if (nb0 + 2LL * P <= total) {
-                // interior chunk (all but the last of a stream): plain coalesced dword loads
-                const uint32_t* src = reinterpret_cast<const uint32_t*>(in + nb0) + tid;
+        if constexpr (PF == 2) {
 #pragma unroll
-                for (int l = 0; l < NLD; l++)
-                    if ((P / 2) % NT == 0 || tid + l * NT < P / 2) pf[l] = src[l * NT];
-            } else {
-#pragma unroll
-                for (int l = 0; l < NLD; l++) {
-                    const int u = tid + l * NT;
-                    if (u < P / 2) pf[l] = load4(in, halo, nb0 + 4LL * u, total, hb);
-                }
-            }
+            for (int l = 0; l < NLD; l++) pf[l] = pf2[l];
+            if (c + 2 < c1) fetch(c + 2, pf2);
+        } else {
+            if (c + 1 < c1) fetch(c + 1, pf);
         }
 
         // ---- RF LPF + decimate.  Thread t owns outputs j = R t + r, r < R, whose samples are
@@ -201,6 +213,7 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         for (int j = 0; j < PD; j++) ldg(j);
 #pragma unroll
         for (int j = 0; j < NG; j++) {
+            if constexpr ((ABL & 1) != 0) break;
             ldg(j + PD);
 #pragma unroll
             for (int h = 0; h < 2; h++) {
@@ -215,6 +228,10 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                 }
             }
             __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+            for (int r = 0; r < R; r++) acc[r] = X[T - 1 + D * r] * cc[0].y;
         }
         // Pin the accumulators here: without it LLVM sinks the pure-register FIR chains past
         // the barrier to their first use (demod), keeping the whole sample window live.
@@ -236,7 +253,10 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const float2v pv = r == 0 ? prev : acc[r - 1];
-            d[r] = fm_demod_one(acc[r].x, acc[r].y, pv.x, pv.y);
+            if constexpr ((ABL & 4) != 0)
+                d[r] = acc[r].x - pv.y;
+            else
+                d[r] = fm_demod_one(acc[r].x, acc[r].y, pv.x, pv.y);
         }
         const long long g0 = c * CIF + R * tid;  // IF index of d[0]
 #pragma unroll
@@ -267,7 +287,7 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                 const float* dw = &dbuf[cur][AD * m - c * CIF + kAH];
                 float a = 0.0f;
 #pragma unroll
-                for (int k = 0; k < kAudioTaps; k++) {
+                for (int k = 0; k < ((ABL & 2) != 0 ? 1 : kAudioTaps); k++) {
                     const float p = atab[k] * dw[-k];
                     a = a + p;
                 }
@@ -280,10 +300,231 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     }
 }
 
-template <int T, int D, int AD, int NT, int R, int PD>
+// ---- single-wave variant with a software-pipelined audio stage -------------------------
+// A 64-thread workgroup is one wave, so its "barriers" are free and lanes can trade values
+// through cross-lane shuffles.  The audio FIR of chunk c-1 (a 51-step dependent chain that
+// would otherwise run alone after the RF stage) is interleaved into chunk c's RF tap loop,
+// APG taps per tap group, where the RF's independent work hides its latency.
+template <int T, int D, int AD, int R, int PD>
+__global__ void __launch_bounds__(64) mono_wave_kernel(MonoLaunch L, MonoTaps taps) {
+    constexpr int NT = 64;
+    using C = MonoCfg<T, D, AD, NT, R>;
+    constexpr int CIF = C::CIF, P = C::P, H = C::H, S = C::S, G = C::G, NLD = C::NLD;
+    constexpr int WH = C::WH, NG = C::NG;
+    constexpr int APG = (kAudioTaps + NG - 1) / NG;  // audio taps per RF tap group
+    static_assert(C::CAmax <= NT, "one audio output per lane per chunk");
+
+    __shared__ float4 xb4[C::XB / 2 + 1];
+    __shared__ float dbuf[2][kAH + CIF];
+    __shared__ float2 ctab2[NG + 1];
+    __shared__ float atab[APG * NG + 1];
+    float2v* xb = reinterpret_cast<float2v*>(xb4);
+    float* ctab = reinterpret_cast<float*>(ctab2);
+
+    const int tid = threadIdx.x;
+    const int stream = blockIdx.x / L.segs;
+    const int seg = blockIdx.x - stream * L.segs;
+    const long long n_if = L.n_if;
+    const long long n_chunks = (n_if + CIF - 1) / CIF;
+    const long long c0 = seg * n_chunks / L.segs;
+    const long long c1 = (seg + 1) * n_chunks / L.segs;
+    if (c0 >= c1) return;
+    const long long n_audio = n_if / AD;
+
+    const uint8_t* in = L.iq + (size_t)stream * L.stream_bytes;
+    const uint8_t* halo = L.halo + (size_t)stream * L.halo_bytes;
+    const long long total = (long long)L.stream_bytes;
+    const long long hb = (long long)L.halo_bytes;
+
+    for (int i = tid; i < 2 * (NG + 1); i += NT) ctab[i] = (i >= 1 && i <= T) ? taps.rf[i - 1] : 0.0f;
+    for (int i = tid; i < APG * NG + 1; i += NT) atab[i] = i < kAudioTaps ? taps.audio[i] : 0.0f;
+    for (int i = tid; i < H / 2; i += NT) {
+        const uint32_t w = load4(in, halo, ((c0 - 1) * (long long)P - H + 2 * i) * 2, total, hb) ^ 0x80808080u;
+        xb4[C::slot(2 * i) / 2] = make_float4(sbyte<0>(w), sbyte<1>(w), sbyte<2>(w), sbyte<3>(w));
+    }
+    uint32_t pf[NLD];
+#pragma unroll
+    for (int l = 0; l < NLD; l++) {
+        const int u = tid + l * NT;
+        if (u < P / 2) pf[l] = load4(in, halo, (c0 - 1) * 2LL * P + 4LL * u, total, hb);
+    }
+
+    // audio output owned by this lane for chunk a: m = ceil(a CIF / AD) + tid
+    auto audio_slot = [&](long long a, bool& active) -> long long {
+        const long long m = (a * CIF + AD - 1) / AD + tid;
+        active = L.audio && a >= c0 && tid < C::CAmax && AD * m < (a + 1) * CIF && m < n_audio;
+        return m;
+    };
+    auto audio_store = [&](long long m, float acc) {
+        const size_t oi = (size_t)stream * (size_t)n_audio + (size_t)m;
+        L.pcm[oi] = quantize_s16(acc);
+        if (L.mono) L.mono[oi] = acc;
+    };
+
+    float2v carry = {0.0f, 0.0f};  // last RF output of the previous chunk (uniform)
+    int cur = 0;
+    for (long long c = c0 - 1; c < c1; c++) {
+#pragma unroll
+        for (int l = 0; l < NLD; l++) {
+            const int u = tid + l * NT;
+            if ((P / 2) % NT == 0 || u < P / 2) {
+                const uint32_t w = pf[l] ^ 0x80808080u;
+                xb4[C::slot(H + 2 * u) / 2] = make_float4(sbyte<0>(w), sbyte<1>(w), sbyte<2>(w), sbyte<3>(w));
+            }
+        }
+        __syncthreads();  // staging (and the previous chunk's demod window) visible
+        if (c + 1 < c1) {
+            const long long nb0 = (c + 1) * 2LL * P;
+            if (nb0 + 2LL * P <= total) {
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(in + nb0) + tid;
+#pragma unroll
+                for (int l = 0; l < NLD; l++)
+                    if ((P / 2) % NT == 0 || tid + l * NT < P / 2) pf[l] = src[l * NT];
+            } else {
+#pragma unroll
+                for (int l = 0; l < NLD; l++) {
+                    const int u = tid + l * NT;
+                    if (u < P / 2) pf[l] = load4(in, halo, nb0 + 4LL * u, total, hb);
+                }
+            }
+        }
+
+        // audio of chunk c-1 (window in dbuf[cur^1]), run inside the RF loop below
+        bool a_on;
+        const long long am = audio_slot(c - 1, a_on);
+        const int aoff = a_on ? (int)(AD * am - (c - 1) * CIF + kAH) : kAH;
+        const float* dw = &dbuf[cur ^ 1][aoff];
+        float aacc = 0.0f;
+
+        float2v acc[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] = float2v{0.0f, 0.0f};
+        int zero;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+        const float2* cb = ctab2 + zero;
+        const float* ab = atab + zero;
+        float2v X[WH + 3];
+        float2 cc[NG];
+        float av[NG * APG], aw[NG * APG];
+        const float4* wb = xb4 + ((S + G) / 2) * tid;
+        auto ld = [&](int o) {
+            const float4 q = wb[(o + G * (o / S)) / 2];
+            X[o] = float2v{q.x, q.y};
+            X[o + 1] = float2v{q.z, q.w};
+        };
+        auto ldg = [&](int j) {
+            if (j < NG) {
+                cc[j] = cb[j];
+                if (j >= 1) ld(T - 1 - 2 * j);
+#pragma unroll
+                for (int h = 0; h < APG; h++) {
+                    const int k = j * APG + h;
+                    if (k < kAudioTaps) {
+                        aw[k] = ab[k];
+                        av[k] = dw[-k];
+                    }
+                }
+            }
+        };
+#pragma unroll
+        for (int o = T - 1; o <= WH; o += 2) ld(o);
+#pragma unroll
+        for (int j = 0; j < PD; j++) ldg(j);
+#pragma unroll
+        for (int j = 0; j < NG; j++) {
+            ldg(j + PD);
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int k = 2 * j - 1 + h;
+                if (k >= 0) {
+                    const float ck = h == 0 ? cc[j].x : cc[j].y;
+#pragma unroll
+                    for (int r = 0; r < R; r++) {
+                        const float2v p = X[T - 1 - k + D * r] * ck;
+                        acc[r] = acc[r] + p;
+                    }
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < APG; h++) {
+                const int k = j * APG + h;
+                if (k < kAudioTaps) {
+                    const float p = aw[k] * av[k];
+                    aacc = aacc + p;
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            asm volatile("" ::"v"(acc[r]));
+            acc[r] = acc[r] * 0.0078125f;
+        }
+        asm volatile("" ::"v"(aacc));
+        if (a_on) audio_store(am, aacc);
+
+        // carries for chunk c+1 (same wave: the RF reads above are complete in order)
+        for (int i = tid; i < H; i += NT) xb[C::slot(i)] = xb[C::slot(P + i)];
+
+        // FM demod: previous output from the neighbouring lane / previous chunk
+        float2v prev;
+        prev.x = __shfl_up(acc[R - 1].x, 1);
+        prev.y = __shfl_up(acc[R - 1].y, 1);
+        if (tid == 0) prev = carry;
+        carry.x = __shfl(acc[R - 1].x, NT - 1);
+        carry.y = __shfl(acc[R - 1].y, NT - 1);
+        float d[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const float2v pv = r == 0 ? prev : acc[r - 1];
+            d[r] = fm_demod_one(acc[r].x, acc[r].y, pv.x, pv.y);
+        }
+        const long long g0 = c * CIF + R * tid;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int jl = R * tid + r;
+            dbuf[cur][kAH + jl] = d[r];
+            if (jl >= CIF - kAH) dbuf[cur ^ 1][jl - (CIF - kAH)] = d[r];
+        }
+        if (c >= c0 && (L.demod || L.demod_tail)) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const long long g = g0 + r;
+                if (g < n_if) {
+                    if (L.demod)
+                        L.demod[(size_t)stream * L.demod_stride + L.demod_hist + g] = d[r];
+                    if (L.demod_tail && g >= n_if - kAH)
+                        L.demod_tail[(size_t)stream * kAH + (g - (n_if - kAH))] = d[r];
+                }
+            }
+        }
+        cur ^= 1;
+    }
+    // epilogue: audio of the last chunk (window in dbuf[cur^1] after the final toggle)
+    __syncthreads();
+    bool a_on;
+    const long long am = audio_slot(c1 - 1, a_on);
+    if (a_on) {
+        const float* dw = &dbuf[cur ^ 1][AD * am - (c1 - 1) * CIF + kAH];
+        float a = 0.0f;
+        for (int k = 0; k < kAudioTaps; k++) {
+            const float p = atab[k] * dw[-k];
+            a = a + p;
+        }
+        audio_store(am, a);
+    }
+}
+
+template <int T, int D, int AD, int R, int PD>
+int launch_wave(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStream_t s) {
+    hipLaunchKernelGGL((mono_wave_kernel<T, D, AD, R, PD>), dim3(n_streams * L.segs), dim3(64), 0, s, L, taps);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+template <int T, int D, int AD, int NT, int R, int PD, int PF = 1>
 int launch_variant(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStream_t s) {
     const dim3 grid(n_streams * L.segs), block(NT);
-    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD>), grid, block, 0, s, L, taps);
+    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD, 0, PF>), grid, block, 0, s, L, taps);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -293,10 +534,11 @@ struct Variant {
     int nt, r, pd, wg_per_cu;  // wg_per_cu: resident workgroups per CU (LDS-limited)
 };
 constexpr Variant kVariants[] = {{256, 3, 3, 2}, {128, 3, 3, 4}, {64, 3, 3, 8}, {128, 5, 3, 3},
-                                 {256, 3, 5, 2}};
+                                 {256, 3, 5, 2}, {64, 3, 3, 8}, {64, 3, 3, 8}, {128, 3, 3, 4}};
+// 5: mono_wave_kernel; 6, 7: input prefetched two chunks ahead
 constexpr int kDefaultVariant = 2;  // 64-thread workgroups: waves never wait on each other
 
-int variant_index() {
+int variant_index() {  // FMRX_MONO_VARIANT: tuning sweeps only
     static int v = [] {
         const char* e = getenv("FMRX_MONO_VARIANT");
         const int i = e ? atoi(e) : kDefaultVariant;
@@ -322,9 +564,36 @@ long long mono_chunks(long long n_if, int /*rf_taps*/, int rf_decim, int /*audio
 
 int mono_wg_per_cu(int rf_decim) { return rf_decim == 9 ? 8 : kVariants[variant_index()].wg_per_cu; }
 
+int ablation() {
+    static int a = [] {
+        const char* e = getenv("FMRX_ABLATE");  // timing experiments only (wrong results)
+        return e ? atoi(e) : 0;
+    }();
+    return a;
+}
+
+template <int ABL>
+int launch_ablation(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStream_t s) {
+    hipLaunchKernelGGL((mono_fused_kernel<101, 10, 5, 64, 3, 3, ABL>), dim3(n_streams * L.segs), dim3(64),
+                       0, s, L, taps);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_decim,
                       int audio_down, const MonoTaps& taps, hipStream_t s) {
     const int vi = variant_index();
+    if (const int a = ablation(); a != 0 && rf_taps == 101 && rf_decim == 10 && vi == 2) {
+        switch (a) {
+            case 1: return launch_ablation<1>(L, n_streams, taps, s);
+            case 2: return launch_ablation<2>(L, n_streams, taps, s);
+            case 4: return launch_ablation<4>(L, n_streams, taps, s);
+            case 8: return launch_ablation<8>(L, n_streams, taps, s);
+            case 6: return launch_ablation<6>(L, n_streams, taps, s);
+            case 14: return launch_ablation<14>(L, n_streams, taps, s);
+            case 15: return launch_ablation<15>(L, n_streams, taps, s);
+            default: break;
+        }
+    }
 #define FMRX_V(T_, D_, AD_, I_, NT_, R_, PD_)                                              \
     if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == I_)                  \
         return launch_variant<T_, D_, AD_, NT_, R_, PD_>(L, n_streams, taps, s);
@@ -333,7 +602,13 @@ int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_de
     FMRX_V(T_, D_, AD_, 1, 128, 3, 3)   \
     FMRX_V(T_, D_, AD_, 2, 64, 3, 3)    \
     FMRX_V(T_, D_, AD_, 3, 128, 5, 3)   \
-    FMRX_V(T_, D_, AD_, 4, 256, 3, 5)
+    FMRX_V(T_, D_, AD_, 4, 256, 3, 5)   \
+    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 5) \
+        return launch_wave<T_, D_, AD_, 3, 3>(L, n_streams, taps, s);    \
+    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 6) \
+        return launch_variant<T_, D_, AD_, 64, 3, 3, 2>(L, n_streams, taps, s); \
+    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 7) \
+        return launch_variant<T_, D_, AD_, 128, 3, 3, 2>(L, n_streams, taps, s);
     FMRX_ALL(51, 10, 5)    // mode 0 (and mode 2's RF stage), reference taps
     FMRX_ALL(101, 10, 5)   // mode 0, 101-tap RF (BASELINE configs[1])
     FMRX_ALL(51, 4, 6)     // mode 1

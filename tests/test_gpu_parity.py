@@ -300,3 +300,22 @@ def test_device_synth_equals_host(fmrx):
         rx.synth_device(9, 123456, 300001, d.data_ptr())
         rx.synchronize()
         assert np.array_equal(d.cpu().numpy(), fmrx.synth_host(9, 2400000, 123456, 300001))
+
+
+# ---- the `project` drop-in CLI (stdin u8 -> stdout S16) --------------------------------------
+
+@pytest.mark.parametrize("mode,channels,batch", [(0, 2, 16), (0, 1, 3), (1, 2, 5), (2, 1, 1)])
+def test_cli_stdin_to_stdout(fmrx, orc, mode, channels, batch):
+    import os
+    import subprocess
+
+    bb, rf_fs = oracle.MODES[mode][0], oracle.MODES[mode][3]
+    nb = {0: 23, 1: 17, 2: 2}[mode]
+    iq = iqgen.make("synth:91", nb * bb + 4321, rf_fs)  # ragged tail is dropped
+    exe = os.path.join(os.path.dirname(fmrx.LIB_PATH), "bin", "fmrx")
+    r = subprocess.run([exe, str(mode), str(channels), "--batch", str(batch)], input=iq.tobytes(),
+                       capture_output=True, timeout=300)
+    assert r.returncode == 0, r.stderr.decode()
+    got = np.frombuffer(r.stdout, np.int16)
+    want = orc.run(mode, 51, iq, ["pcm", "pcm_mono"])["pcm" if channels == 2 else "pcm_mono"]
+    assert np.array_equal(got, want)
