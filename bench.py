@@ -34,6 +34,17 @@ STREAM_BYTES = 1 << 30         # BASELINE config 2: 1 GiB synthetic IQ
 RF_TAPS = 101
 
 
+# compiled variants of the fused kernel (csrc/mono_fused.hip kVariants), default index 2
+_VARIANTS = ["mono_fused_kernel<101,10,5,256,3,3>", "mono_fused_kernel<101,10,5,128,3,3>",
+             "mono_fused_kernel<101,10,5,64,3,3>", "mono_fused_kernel<101,10,5,128,5,3>",
+             "mono_fused_kernel<101,10,5,256,3,5>", "mono_wave_kernel<101,10,5,3,3>",
+             "mono_fused_kernel<101,10,5,64,3,3,PF=2>", "mono_fused_kernel<101,10,5,128,3,3,PF=2>"]
+
+
+def kernel_name() -> str:
+    return _VARIANTS[int(os.environ.get("FMRX_MONO_VARIANT", "2"))]
+
+
 def flops_per_iq(rf_taps: int) -> float:
     # per IQ pair: RF 2 ch x taps x (mul+add) / 10, demod ~9/10, audio 51x2/50
     return 2 * rf_taps * 2 / 10 + 0.9 + 51 * 2 / 50
@@ -132,7 +143,7 @@ def main() -> None:
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
-            "kernel": "mono_fused_kernel<101,10,5,256,3>",
+            "kernel": kernel_name(),
             "kernel_ms": round(kern_ms, 4),
             "launches_timed": launches,
             "alg_bytes_per_launch": alg_bytes,
