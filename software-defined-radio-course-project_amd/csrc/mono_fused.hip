@@ -137,6 +137,11 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     uint32_t pf[NLD], pf2[NLD];
     auto fetch = [&](long long cc, uint32_t (&dst)[NLD]) {
         const long long nb0 = cc * 2LL * P;  // first byte of chunk cc
+        if constexpr ((ABL & 16) != 0) {  // ablation: no global loads
+#pragma unroll
+            for (int l = 0; l < NLD; l++) dst[l] = (uint32_t)(nb0 + l * 77 + tid);
+            return;
+        }
         if (nb0 >= 0 && nb0 + 2LL * P <= total) {
             // interior chunk (all but the ends of a stream): plain coalesced dword loads
             const uint32_t* src = reinterpret_cast<const uint32_t*>(in + nb0) + tid;
@@ -165,6 +170,10 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
             const int u = tid + l * NT;
             if ((P / 2) % NT == 0 || u < P / 2) {
                 const uint32_t w = pf[l] ^ 0x80808080u;
+                if constexpr ((ABL & 32) != 0) {  // ablation: no staging writes
+                    asm volatile("" ::"v"(w));
+                    continue;
+                }
                 if constexpr ((ABL & 8) != 0)
                     xb4[C::slot(H + 2 * u) / 2] = make_float4(__uint_as_float(w), 0.f, 0.f, 0.f);
                 else
@@ -591,6 +600,10 @@ int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_de
             case 6: return launch_ablation<6>(L, n_streams, taps, s);
             case 14: return launch_ablation<14>(L, n_streams, taps, s);
             case 15: return launch_ablation<15>(L, n_streams, taps, s);
+            case 16: return launch_ablation<16>(L, n_streams, taps, s);
+            case 31: return launch_ablation<31>(L, n_streams, taps, s);
+            case 47: return launch_ablation<47>(L, n_streams, taps, s);
+            case 63: return launch_ablation<63>(L, n_streams, taps, s);
             default: break;
         }
     }
