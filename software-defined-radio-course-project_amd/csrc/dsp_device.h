@@ -22,11 +22,11 @@ __host__ __device__ inline float fm_demod_one(float ci, float cq, float pi, floa
     const float dq = cq - pq;
     const float den = static_cast<float>(static_cast<double>(ci) * static_cast<double>(ci) +
                                          static_cast<double>(cq) * static_cast<double>(cq));
-    if (den != 0.0f) {
-        const float num = (ci * dq) - (cq * di);
-        return num / den;
-    }
-    return 0.0f;
+    // The quotient is formed unconditionally and selected (no divergent branch on device);
+    // den == 0 gives 0 exactly as filter.cpp:125-129.
+    const float num = (ci * dq) - (cq * di);
+    const float q = num / den;
+    return den != 0.0f ? q : 0.0f;
 }
 
 // src/project.cpp:185-191: NaN -> 0, else static_cast<short>(x * 16384) as the x86-64 build

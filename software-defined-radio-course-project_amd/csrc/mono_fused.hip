@@ -96,27 +96,40 @@ __device__ inline float sbyte(uint32_t w) {
 
 // ABL (timing ablations only, never selected in production): bit 1 skips the RF FIR, 2 the
 // audio FIR, 4 the demod, 8 the byte conversion of the staging.
-template <int T, int D, int AD, int NT, int R, int PD, int ABL = 0, int PF = 1>
+// TR = 1 keeps the RF taps in VGPRs for the whole launch (the kernel is LDS-capped at two
+// waves per SIMD, which leaves the register file room for them) instead of re-reading them
+// from LDS once per chunk.
+// AK = 2 (single-wave workgroups only) runs the audio stage once per pair of chunks: each
+// lane then owns two outputs, m and m + NB, accumulated together in packed f32 ops, which
+// halves the audio stage's instructions; the neighbour I/Q for the demod comes by lane
+// shuffle instead of LDS, which pays for the larger demod window.
+template <int T, int D, int AD, int NT, int R, int PD, int ABL = 0, int PF = 1, int TR = 0, int AK = 1>
 __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps taps) {
     using C = MonoCfg<T, D, AD, NT, R>;
     constexpr int CIF = C::CIF, P = C::P, H = C::H, S = C::S, G = C::G, NLD = C::NLD;
     constexpr int WH = C::WH, NG = C::NG;
+    static_assert(AK == 1 || (AK == 2 && NT == 64 && CIF >= kAH), "grouped audio: one wave, CIF >= 50");
+    constexpr int NB = ((2 * CIF + AD - 1) / AD + 1) / 2;  // AK = 2: output pairs per group
+    static_assert(AK == 1 || NB <= NT, "one output pair per lane");
 
     __shared__ float4 xb4[C::XB / 2 + 1];        // scaled (I,Q) pairs, two per float4
-    __shared__ float dbuf[2][kAH + CIF];         // demod window: 50 history + chunk
-    __shared__ float2v pbuf[2][NT + 1];          // last RF output of each thread (+carry)
+    __shared__ float dbuf[2][kAH + AK * CIF];    // demod window: 50 history + AK chunks
+    __shared__ float2v pbuf[AK == 1 ? 2 : 1][AK == 1 ? NT + 1 : 1];  // last RF output per thread
     __shared__ float2 ctab2[NG + 1];             // (c[2j-1], c[2j]); c[-1] = 0
     __shared__ float atab[kAudioTaps + 1];       // audio taps
-    float2v* xb = reinterpret_cast<float2v*>(xb4);
     float* ctab = reinterpret_cast<float*>(ctab2);
 
     const int tid = threadIdx.x;
     const int stream = blockIdx.x / L.segs;
     const int seg = blockIdx.x - stream * L.segs;
     const long long n_if = L.n_if;
-    const long long n_chunks = (n_if + CIF - 1) / CIF;
-    const long long c0 = seg * n_chunks / L.segs;
-    const long long c1 = (seg + 1) * n_chunks / L.segs;
+    // chunk indices fit 32 bits for any HBM-resident stream (n_if / CIF < 2^31); positions
+    // in the stream stay 64-bit
+    const int n_chunks = (int)((n_if + CIF - 1) / CIF);
+    const int c0 = (int)((long long)seg * n_chunks / L.segs);
+    const int c1 = (int)((long long)(seg + 1) * n_chunks / L.segs);
+    const int c_full = (int)(L.stream_bytes / (2 * P));  // chunks lying wholly in the data
+    const int c_tail = n_if >= kAH ? (int)((n_if - kAH) / CIF) : -2;  // chunks holding the last 50
     if (c0 >= c1) return;
     const long long n_audio = n_if / AD;
 
@@ -130,46 +143,59 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
 
     // ---- prologue: RF history in front of the pre-roll chunk (pairs [(c0-1)P - H, (c0-1)P))
     for (int i = tid; i < H / 2; i += NT) {
-        const uint32_t w = load4(in, halo, ((c0 - 1) * (long long)P - H + 2 * i) * 2, total, hb) ^ 0x80808080u;
+        const uint32_t w = load4(in, halo, ((long long)(c0 - 1) * P - H + 2 * i) * 2, total, hb) ^ 0x80808080u;
         xb4[C::slot(2 * i) / 2] = make_float4(sbyte<0>(w), sbyte<1>(w), sbyte<2>(w), sbyte<3>(w));
     }
     // Input prefetch, PF chunks ahead: pf holds chunk c, pf2 (PF == 2) chunk c+1.
     uint32_t pf[NLD], pf2[NLD];
-    auto fetch = [&](long long cc, uint32_t (&dst)[NLD]) {
-        const long long nb0 = cc * 2LL * P;  // first byte of chunk cc
+    // The prefetch is always the same coalesced dword loads, from a base clamped into the
+    // stream so that they never leave it; the few chunks that touch the halo or run past the
+    // end (c outside [0, c_full)) are rebuilt at staging time instead.  One load path keeps
+    // the loads asynchronous: with a second path the compiler merges the two sets of
+    // registers right after issue, behind an s_waitcnt that exposes the HBM latency.
+    auto fetch = [&](int cc, uint32_t (&dst)[NLD]) {
         if constexpr ((ABL & 16) != 0) {  // ablation: no global loads
 #pragma unroll
-            for (int l = 0; l < NLD; l++) dst[l] = (uint32_t)(nb0 + l * 77 + tid);
+            for (int l = 0; l < NLD; l++) dst[l] = (uint32_t)(cc * 77 + l * 77 + tid);
             return;
         }
-        if (nb0 >= 0 && nb0 + 2LL * P <= total) {
-            // interior chunk (all but the ends of a stream): plain coalesced dword loads
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(in + nb0) + tid;
+        if (c_full == 0) return;  // stream shorter than a chunk: every chunk is rebuilt
+        const int cl = cc < 0 ? 0 : (cc < c_full ? cc : c_full - 1);
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(in + (size_t)cl * (2 * P)) + tid;
 #pragma unroll
-            for (int l = 0; l < NLD; l++)
-                if ((P / 2) % NT == 0 || tid + l * NT < P / 2) dst[l] = src[l * NT];
-        } else {
-#pragma unroll
-            for (int l = 0; l < NLD; l++) {
-                const int u = tid + l * NT;
-                if (u < P / 2) dst[l] = load4(in, halo, nb0 + 4LL * u, total, hb);
-            }
-        }
+        for (int l = 0; l < NLD; l++)
+            if ((P / 2) % NT == 0 || tid + l * NT < P / 2) dst[l] = src[l * NT];
     };
     fetch(c0 - 1, pf);
     if constexpr (PF == 2) {
         if (c0 < c1) fetch(c0, pf2);
     }
 
+    float2 creg[TR ? NG : 1];
+    if constexpr (TR != 0) {
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < NG; j++) creg[j] = ctab2[j];
+    }
     int cur = 0;
-    for (long long c = c0 - 1; c < c1; c++) {
+    // (c0-1) CIF = AD aq + ar; for c0 = 0 this is (-(CIF/AD), -(CIF%AD)), which the first
+    // increment turns into (0, 0), and ar is only read for c >= c0.
+    long long aq = (long long)(c0 - 1) * CIF / AD;
+    int ar = (int)((long long)(c0 - 1) * CIF - aq * AD);
+    long long gaq = 0;  // AK = 2: (aq, ar) of the current group's first audio chunk
+    int gar = 0;
+    float2v carry = {0.0f, 0.0f};  // AK = 2: last RF output of the previous chunk
+    for (int c = c0 - 1; c < c1; c++) {
         // ---- stage chunk c: lane u writes pairs H+2u, H+2u+1 as one float4; consecutive
         // lanes write consecutive 16-B slots (conflict-free ds_write_b128).
+        const bool edge = (ABL & 16) == 0 && !(c >= 0 && c < c_full);
 #pragma unroll
         for (int l = 0; l < NLD; l++) {
             const int u = tid + l * NT;
             if ((P / 2) % NT == 0 || u < P / 2) {
-                const uint32_t w = pf[l] ^ 0x80808080u;
+                uint32_t raw = pf[l];
+                if (edge) raw = load4(in, halo, (long long)c * (2 * P) + 4LL * u, total, hb);
+                const uint32_t w = raw ^ 0x80808080u;
                 if constexpr ((ABL & 32) != 0) {  // ablation: no staging writes
                     asm volatile("" ::"v"(w));
                     continue;
@@ -196,6 +222,12 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         // thread) and taps come as broadcast LDS pairs.  Group 0 = tap 0, group j = taps
         // 2j-1, 2j; group j's new samples are the pair (T-1-2j, T-2j); loads run PD groups
         // ahead of use.
+        if constexpr (TR != 0) {
+            // Opaque per chunk, so LICM cannot hoist 101 loop-invariant (c, c) splats out of
+            // the chunk loop; the products then broadcast a tap with op_sel instead.
+#pragma unroll
+            for (int j = 0; j < NG; j++) asm volatile("" : "+v"(creg[j]));
+        }
         float2v acc[R];
 #pragma unroll
         for (int r = 0; r < R; r++) acc[r] = float2v{0.0f, 0.0f};
@@ -212,7 +244,7 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         };
         auto ldg = [&](int j) {  // loads of group j
             if (j < NG) {
-                cc[j] = cb[j];
+                if constexpr (TR == 0) cc[j] = cb[j];
                 if (j >= 1) ld(T - 1 - 2 * j);
             }
         };
@@ -228,7 +260,8 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
             for (int h = 0; h < 2; h++) {
                 const int k = 2 * j - 1 + h;
                 if (k >= 0) {
-                    const float ck = h == 0 ? cc[j].x : cc[j].y;
+                    const float2 cj = TR ? creg[TR ? j : 0] : cc[j];
+                    const float ck = h == 0 ? cj.x : cj.y;
 #pragma unroll
                     for (int r = 0; r < R; r++) {
                         const float2v p = X[T - 1 - k + D * r] * ck;
@@ -240,7 +273,7 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         }
         if constexpr ((ABL & 1) != 0) {
 #pragma unroll
-            for (int r = 0; r < R; r++) acc[r] = X[T - 1 + D * r] * cc[0].y;
+            for (int r = 0; r < R; r++) acc[r] = X[T - 1 + D * r] * (TR ? creg[0].y : cc[0].y);
         }
         // Pin the accumulators here: without it LLVM sinks the pure-register FIR chains past
         // the barrier to their first use (demod), keeping the whole sample window live.
@@ -249,15 +282,23 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
             asm volatile("" ::"v"(acc[r]));
             acc[r] = acc[r] * 0.0078125f;  // undo the 2^7 sample scaling (exact)
         }
-        pbuf[cur][tid + 1] = acc[R - 1];
+        if constexpr (AK == 1) pbuf[cur][tid + 1] = acc[R - 1];
         __syncthreads();  // (B) all RF reads of xb done, pbuf visible
 
-        // ---- carries for chunk c+1: RF history (pairs [P, P+H) -> [0, H)), last I/Q
-        for (int i = tid; i < H; i += NT) xb[C::slot(i)] = xb[C::slot(P + i)];
-        if (tid == 0) pbuf[cur ^ 1][0] = pbuf[cur][NT];
-
-        // ---- FM demod (prev from the neighbouring thread / previous chunk)
-        const float2v prev = pbuf[cur][tid];
+        // ---- carries for chunk c+1: RF history (pairs [P, P+H) -> [0, H)) as aligned 16-B
+        // pair groups (P and H are even, so groups never straddle a pad), last I/Q
+        for (int i = tid; i < H / 2; i += NT) xb4[C::slot(2 * i) / 2] = xb4[C::slot(P + 2 * i) / 2];
+        float2v prev;
+        if constexpr (AK == 1) {
+            if (tid == 0) pbuf[cur ^ 1][0] = pbuf[cur][NT];
+            prev = pbuf[cur][tid];  // FM demod's previous I/Q: neighbouring thread / chunk
+        } else {
+            prev.x = __shfl_up(acc[R - 1].x, 1);
+            prev.y = __shfl_up(acc[R - 1].y, 1);
+            if (tid == 0) prev = carry;
+            carry.x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc[R - 1].x), NT - 1));
+            carry.y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc[R - 1].y), NT - 1));
+        }
         float d[R];
 #pragma unroll
         for (int r = 0; r < R; r++) {
@@ -267,14 +308,19 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
             else
                 d[r] = fm_demod_one(acc[r].x, acc[r].y, pv.x, pv.y);
         }
-        const long long g0 = c * CIF + R * tid;  // IF index of d[0]
+        const long long g0 = (long long)c * CIF + R * tid;  // IF index of d[0]
+        // AK = 2: chunk c is slot q of its group (groups start at the pre-roll chunk); the
+        // group's last 50 samples also go to the other buffer as the next group's history.
+        const int q = AK == 1 ? 0 : (int)((c - (c0 - 1)) & 1);
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const int jl = R * tid + r;
-            dbuf[cur][kAH + jl] = d[r];
-            if (jl >= CIF - kAH) dbuf[cur ^ 1][jl - (CIF - kAH)] = d[r];
+            dbuf[cur][kAH + q * CIF + jl] = d[r];
+            if ((AK == 1 || q == 1) && jl >= CIF - kAH) dbuf[cur ^ 1][jl - (CIF - kAH)] = d[r];
         }
-        if (c >= c0) {
+        // Demod to global only for the split API / the chunk holding the stream's last 50
+        // samples (one scalar test per chunk; the fused mono path skips it otherwise).
+        if (c >= c0 && (L.demod || (L.demod_tail && c >= c_tail))) {
 #pragma unroll
             for (int r = 0; r < R; r++) {
                 const long long g = g0 + r;
@@ -289,11 +335,48 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         __syncthreads();  // (C) demod window complete
 
         // ---- audio LPF + decimate + quantise: outputs m with AD*m in this chunk
-        if (L.audio && c >= c0) {
-            const long long m0 = (c * CIF + AD - 1) / AD;
-            const long long m = m0 + tid;
-            if (tid < C::CAmax && AD * m < (c + 1) * CIF && m < n_audio) {
-                const float* dw = &dbuf[cur][AD * m - c * CIF + kAH];
+        // Chunk c starts at IF index pos = c CIF = AD aq + ar (tracked incrementally); its
+        // first audio output is m0 = aq + (ar > 0), at chunk offset off0 = AD m0 - pos.
+        if constexpr (AK == 2) {
+            // group audio start: chunk gs = max(cs, c0), where cs = c - q starts the group
+            if (c >= c0 && (q == 0 || c == c0)) { gaq = aq; gar = ar; }
+            if (L.audio && c >= c0 && (q == 1 || c == c1 - 1)) {
+                const int gsrel = (c - q < c0) ? 1 : 0;          // gs - cs
+                const int off0 = gar > 0 ? AD - gar : 0;
+                const long long m0 = gaq + (gar > 0);
+                const int span = (q + 1 - gsrel) * CIF;          // IF samples with audio
+                const long long left = n_audio - m0;
+                const int cnt = (int)std::min<long long>((span - off0 + AD - 1) / AD, left);
+                if (tid < NB && cnt > 0) {
+                    // clamp idle lanes onto valid samples; their sums are not stored
+                    const int ia = kAH + gsrel * CIF + off0 + AD * min(tid, cnt - 1);
+                    const float* dw = &dbuf[cur][ia];
+                    const int db = AD * (min(NB + tid, cnt - 1) - min(tid, cnt - 1));
+                    float2v a2 = {0.0f, 0.0f};
+#pragma unroll
+                    for (int k = 0; k < ((ABL & 2) != 0 ? 1 : kAudioTaps); k++) {
+                        const float2v p = float2v{dw[-k], dw[db - k]} * atab[k];
+                        a2 = a2 + p;
+                    }
+                    const size_t oi = (size_t)stream * (size_t)n_audio + (size_t)m0 + tid;
+                    if (tid < cnt) {
+                        L.pcm[oi] = quantize_s16(a2.x);
+                        if (L.mono) L.mono[oi] = a2.x;
+                    }
+                    if (NB + tid < cnt) {
+                        L.pcm[oi + NB] = quantize_s16(a2.y);
+                        if (L.mono) L.mono[oi + NB] = a2.y;
+                    }
+                }
+            }
+            if (q == 1) cur ^= 1;
+        } else if (L.audio && c >= c0) {
+            const int off0 = ar > 0 ? AD - ar : 0;
+            const long long m0 = aq + (ar > 0);
+            const long long left = n_audio - m0;  // outputs of the stream not yet written
+            if (tid < C::CAmax && off0 + AD * tid < CIF && tid < left) {
+                const long long m = m0 + tid;
+                const float* dw = &dbuf[cur][off0 + AD * tid + kAH];
                 float a = 0.0f;
 #pragma unroll
                 for (int k = 0; k < ((ABL & 2) != 0 ? 1 : kAudioTaps); k++) {
@@ -305,7 +388,10 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                 if (L.mono) L.mono[oi] = a;
             }
         }
-        cur ^= 1;
+        if constexpr (AK == 1) cur ^= 1;
+        aq += CIF / AD;
+        ar += CIF % AD;
+        if (ar >= AD) { ar -= AD; aq++; }
     }
 }
 
@@ -321,6 +407,8 @@ __global__ void __launch_bounds__(64) mono_wave_kernel(MonoLaunch L, MonoTaps ta
     constexpr int CIF = C::CIF, P = C::P, H = C::H, S = C::S, G = C::G, NLD = C::NLD;
     constexpr int WH = C::WH, NG = C::NG;
     constexpr int APG = (kAudioTaps + NG - 1) / NG;  // audio taps per RF tap group
+    constexpr int TR = 0;                             // taps re-read from LDS (see fused kernel)
+    float2 creg[1] = {};
     static_assert(C::CAmax <= NT, "one audio output per lane per chunk");
 
     __shared__ float4 xb4[C::XB / 2 + 1];
@@ -423,7 +511,7 @@ __global__ void __launch_bounds__(64) mono_wave_kernel(MonoLaunch L, MonoTaps ta
         };
         auto ldg = [&](int j) {
             if (j < NG) {
-                cc[j] = cb[j];
+                if constexpr (TR == 0) cc[j] = cb[j];
                 if (j >= 1) ld(T - 1 - 2 * j);
 #pragma unroll
                 for (int h = 0; h < APG; h++) {
@@ -446,7 +534,8 @@ __global__ void __launch_bounds__(64) mono_wave_kernel(MonoLaunch L, MonoTaps ta
             for (int h = 0; h < 2; h++) {
                 const int k = 2 * j - 1 + h;
                 if (k >= 0) {
-                    const float ck = h == 0 ? cc[j].x : cc[j].y;
+                    const float2 cj = TR ? creg[TR ? j : 0] : cc[j];
+                    const float ck = h == 0 ? cj.x : cj.y;
 #pragma unroll
                     for (int r = 0; r < R; r++) {
                         const float2v p = X[T - 1 - k + D * r] * ck;
@@ -530,10 +619,10 @@ int launch_wave(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStr
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-template <int T, int D, int AD, int NT, int R, int PD, int PF = 1>
+template <int T, int D, int AD, int NT, int R, int PD, int PF = 1, int TR = 0, int AK = 1>
 int launch_variant(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStream_t s) {
     const dim3 grid(n_streams * L.segs), block(NT);
-    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD, 0, PF>), grid, block, 0, s, L, taps);
+    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD, 0, PF, TR, AK>), grid, block, 0, s, L, taps);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -543,9 +632,11 @@ struct Variant {
     int nt, r, pd, wg_per_cu;  // wg_per_cu: resident workgroups per CU (LDS-limited)
 };
 constexpr Variant kVariants[] = {{256, 3, 3, 2}, {128, 3, 3, 4}, {64, 3, 3, 8}, {128, 5, 3, 3},
-                                 {256, 3, 5, 2}, {64, 3, 3, 8}, {64, 3, 3, 8}, {128, 3, 3, 4}};
+                                 {256, 3, 5, 2}, {64, 3, 3, 8}, {64, 3, 3, 8}, {128, 3, 3, 4},
+                                 {64, 3, 3, 8}, {64, 3, 4, 8},  // 8, 9: taps in VGPRs
+                                 {64, 3, 4, 8}, {64, 3, 4, 8}};  // 10: + paired audio; 11: paired audio
 // 5: mono_wave_kernel; 6, 7: input prefetched two chunks ahead
-constexpr int kDefaultVariant = 2;  // 64-thread workgroups: waves never wait on each other
+constexpr int kDefaultVariant = 9;  // 64-thread workgroups (waves never wait on each other), taps in VGPRs
 
 int variant_index() {  // FMRX_MONO_VARIANT: tuning sweeps only
     static int v = [] {
@@ -583,15 +674,15 @@ int ablation() {
 
 template <int ABL>
 int launch_ablation(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStream_t s) {
-    hipLaunchKernelGGL((mono_fused_kernel<101, 10, 5, 64, 3, 3, ABL>), dim3(n_streams * L.segs), dim3(64),
-                       0, s, L, taps);
+    hipLaunchKernelGGL((mono_fused_kernel<101, 10, 5, 64, 3, 4, ABL, 1, 1>), dim3(n_streams * L.segs),
+                       dim3(64), 0, s, L, taps);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_decim,
                       int audio_down, const MonoTaps& taps, hipStream_t s) {
     const int vi = variant_index();
-    if (const int a = ablation(); a != 0 && rf_taps == 101 && rf_decim == 10 && vi == 2) {
+    if (const int a = ablation(); a != 0 && rf_taps == 101 && rf_decim == 10) {
         switch (a) {
             case 1: return launch_ablation<1>(L, n_streams, taps, s);
             case 2: return launch_ablation<2>(L, n_streams, taps, s);
@@ -604,6 +695,8 @@ int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_de
             case 31: return launch_ablation<31>(L, n_streams, taps, s);
             case 47: return launch_ablation<47>(L, n_streams, taps, s);
             case 63: return launch_ablation<63>(L, n_streams, taps, s);
+            case 62: return launch_ablation<62>(L, n_streams, taps, s);
+            case 30: return launch_ablation<30>(L, n_streams, taps, s);
             default: break;
         }
     }
@@ -621,7 +714,15 @@ int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_de
     if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 6) \
         return launch_variant<T_, D_, AD_, 64, 3, 3, 2>(L, n_streams, taps, s); \
     if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 7) \
-        return launch_variant<T_, D_, AD_, 128, 3, 3, 2>(L, n_streams, taps, s);
+        return launch_variant<T_, D_, AD_, 128, 3, 3, 2>(L, n_streams, taps, s); \
+    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 8) \
+        return launch_variant<T_, D_, AD_, 64, 3, 3, 1, 1>(L, n_streams, taps, s); \
+    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 9) \
+        return launch_variant<T_, D_, AD_, 64, 3, 4, 1, 1>(L, n_streams, taps, s); \
+    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 10) \
+        return launch_variant<T_, D_, AD_, 64, 3, 4, 1, 1, 2>(L, n_streams, taps, s); \
+    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 11) \
+        return launch_variant<T_, D_, AD_, 64, 3, 4, 1, 0, 2>(L, n_streams, taps, s);
     FMRX_ALL(51, 10, 5)    // mode 0 (and mode 2's RF stage), reference taps
     FMRX_ALL(101, 10, 5)   // mode 0, 101-tap RF (BASELINE configs[1])
     FMRX_ALL(51, 4, 6)     // mode 1
