@@ -40,7 +40,8 @@ _VARIANTS = ["mono_fused_kernel<101,10,5,256,3,3>", "mono_fused_kernel<101,10,5,
              "mono_fused_kernel<101,10,5,256,3,5>", "mono_wave_kernel<101,10,5,3,3>",
              "mono_fused_kernel<101,10,5,64,3,3,PF=2>", "mono_fused_kernel<101,10,5,128,3,3,PF=2>",
              "mono_fused_kernel<101,10,5,64,3,3,TR=1>", "mono_fused_kernel<101,10,5,64,3,4,TR=1>",
-             "mono_fused_kernel<101,10,5,64,3,4,TR=1,AK=2>", "mono_fused_kernel<101,10,5,64,3,4,AK=2>"]
+             "mono_fused_kernel<101,10,5,64,3,4,TR=1,AK=2>", "mono_fused_kernel<101,10,5,64,3,4,AK=2>",
+             "mono_fused_kernel<101,10,5,64,2,4,DB1=1>", "mono_fused_kernel<101,10,5,64,2,3,DB1=1>"]
 
 
 def kernel_name() -> str:

@@ -1,14 +1,25 @@
-// cli.cpp — `fmrx [mode channels] [--batch N] [--device D]`: the drop-in for the reference's
-// `project` executable (src/project.cpp:273-390).  Reads u8 I/Q from stdin, writes raw S16LE
-// to stdout: stereo = 2 channels interleaved R,L exactly like project.cpp:179-195; mono =
-// 1 channel (the private-history mono product; project.cpp logs `channels` but ignores it).
+// cli.cpp — `fmrx [mode channels] [--batch N] [--device D] [--rf-taps T]`: the drop-in for the
+// reference's `project` executable (src/project.cpp:273-390).  Reads u8 I/Q from stdin, writes
+// raw S16LE to stdout: stereo = 2 channels interleaved R,L exactly like project.cpp:179-195;
+// mono = 1 channel (the private-history mono product; project.cpp logs `channels` but ignores
+// it).
 //
-// Threading mirrors project.cpp's producer/consumer split: a reader thread fills batches of
-// whole blocks into a bounded queue of depth 3 (QUEUE_CAPACITY, project.cpp:17) and the main
-// thread runs each batch through libfmrx on the GPU and writes the PCM.  Unlike the reference
-// (project.cpp:51-54, which exit(1)s while blocks are still queued) every full block read is
-// processed before the process exits 0; a trailing partial block is dropped, as in the
-// reference.
+// Streaming runtime.  The reference splits the work into a producer thread
+// (read + RF front end, project.cpp:48-84) and a consumer thread (audio back end, :132-196)
+// joined by a bounded queue of depth 3 (QUEUE_CAPACITY, :17).  Here the whole receive runs on
+// the GPU and the queue becomes a ring of 3 batch slots, each a pinned host input/output pair
+// and a device input/output pair, cycled by three agents:
+//   reader thread : fread whole blocks straight into a free slot's pinned input;
+//   main thread   : H2D on a copy stream -> (event) -> fmrx_process_device on the context's
+//                   stream -> (event) -> D2H on an output stream, all asynchronous;
+//   writer thread : waits for the slot's D2H event, writes its PCM, frees the slot.
+// so the upload of batch i+1, the receive of batch i and the write of batch i-1 overlap.
+// Stream order keeps the receiver state sequential (one context, one compute stream).
+// Unlike the reference (project.cpp:51-54, which exit(1)s while blocks are still queued) every
+// full block read is processed before the process exits 0; a trailing partial block is
+// dropped, as in the reference.
+#include <hip/hip_runtime_api.h>
+
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -22,35 +33,37 @@
 
 namespace {
 
-struct Batch {
-    std::vector<uint8_t> bytes;
-    size_t blocks = 0;
-    bool last = false;
-};
+constexpr int kSlots = 3;  // project.cpp:17 QUEUE_CAPACITY
 
-class BoundedQueue {
+class IndexQueue {
   public:
-    explicit BoundedQueue(size_t cap) : cap_(cap) {}
-    void push(Batch&& b) {
-        std::unique_lock<std::mutex> lk(m_);
-        cv_.wait(lk, [&] { return q_.size() < cap_; });
-        q_.push_back(std::move(b));
+    void push(int v) {
+        std::lock_guard<std::mutex> lk(m_);
+        q_.push_back(v);
         cv_.notify_all();
     }
-    Batch pop() {
+    int pop() {
         std::unique_lock<std::mutex> lk(m_);
         cv_.wait(lk, [&] { return !q_.empty(); });
-        Batch b = std::move(q_.front());
+        const int v = q_.front();
         q_.pop_front();
-        cv_.notify_all();
-        return b;
+        return v;
     }
 
   private:
-    size_t cap_;
     std::mutex m_;
     std::condition_variable cv_;
-    std::deque<Batch> q_;
+    std::deque<int> q_;
+};
+
+struct Slot {
+    uint8_t* h_in = nullptr;   // pinned
+    int16_t* h_out = nullptr;  // pinned
+    uint8_t* d_in = nullptr;
+    int16_t* d_out = nullptr;
+    hipEvent_t uploaded{}, computed{}, downloaded{};
+    size_t blocks = 0;
+    bool last = false;
 };
 
 void usage(const char* argv0) {
@@ -59,6 +72,18 @@ void usage(const char* argv0) {
                  "\t<mode> is a value from 0 to 3, <channels> is either 1 or 2\n",
                  argv0);
 }
+
+[[noreturn]] void die_hip(hipError_t e, const char* what) {
+    std::fprintf(stderr, "fmrx: %s: %s\n", what, hipGetErrorString(e));
+    std::fflush(stdout);
+    std::_Exit(1);
+}
+
+#define CLI_HIP(x)                              \
+    do {                                        \
+        const hipError_t e_ = (x);              \
+        if (e_ != hipSuccess) die_hip(e_, #x);  \
+    } while (0)
 
 }  // namespace
 
@@ -99,47 +124,92 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "fmrx: %s\n", fmrx_last_error());
         return 1;
     }
+    const size_t in_cap = geo.block_bytes * (size_t)batch;
+    const size_t out_cap = geo.pcm_samples * (size_t)batch;
 
-    BoundedQueue queue(3);
+    CLI_HIP(hipSetDevice(device));
+    hipStream_t compute = static_cast<hipStream_t>(fmrx_stream(ctx));
+    hipStream_t up, down;
+    CLI_HIP(hipStreamCreateWithFlags(&up, hipStreamNonBlocking));
+    CLI_HIP(hipStreamCreateWithFlags(&down, hipStreamNonBlocking));
+    Slot slots[kSlots];
+    for (Slot& s : slots) {
+        CLI_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.h_in), in_cap, hipHostMallocDefault));
+        CLI_HIP(hipHostMalloc(reinterpret_cast<void**>(&s.h_out), out_cap * sizeof(int16_t), hipHostMallocDefault));
+        CLI_HIP(hipMalloc(reinterpret_cast<void**>(&s.d_in), in_cap));
+        CLI_HIP(hipMalloc(reinterpret_cast<void**>(&s.d_out), out_cap * sizeof(int16_t)));
+        CLI_HIP(hipEventCreateWithFlags(&s.uploaded, hipEventDisableTiming));
+        CLI_HIP(hipEventCreateWithFlags(&s.computed, hipEventDisableTiming));
+        CLI_HIP(hipEventCreateWithFlags(&s.downloaded, hipEventDisableTiming));
+    }
+
+    IndexQueue free_q, filled_q, done_q;
+    for (int i = 0; i < kSlots; i++) free_q.push(i);
+
     std::thread reader([&] {
         for (;;) {
-            Batch b;
-            b.bytes.resize(geo.block_bytes * (size_t)batch);
+            const int i = free_q.pop();
+            Slot& s = slots[i];
             size_t got = 0;
-            while (got < b.bytes.size()) {
-                const size_t r = std::fread(b.bytes.data() + got, 1, b.bytes.size() - got, stdin);
+            while (got < in_cap) {
+                const size_t r = std::fread(s.h_in + got, 1, in_cap - got, stdin);
                 if (r == 0) break;
                 got += r;
             }
-            b.blocks = got / geo.block_bytes;
-            b.last = got < b.bytes.size();
-            queue.push(std::move(b));
-            if (got < geo.block_bytes * (size_t)batch) return;
+            s.blocks = got / geo.block_bytes;
+            s.last = got < in_cap;
+            filled_q.push(i);
+            if (s.last) return;
+        }
+    });
+    std::thread writer([&] {
+        for (;;) {
+            const int i = done_q.pop();
+            Slot& s = slots[i];
+            if (s.blocks > 0) {
+                CLI_HIP(hipEventSynchronize(s.downloaded));
+                std::fwrite(s.h_out, sizeof(int16_t), s.blocks * geo.pcm_samples, stdout);
+            }
+            if (s.last) return;
+            free_q.push(i);
         }
     });
 
-    int rc = 0;
-    std::vector<int16_t> pcm;
     for (;;) {
-        Batch b = queue.pop();
-        if (b.blocks > 0) {
-            pcm.resize(b.blocks * geo.pcm_samples);
-            if (fmrx_process(ctx, b.bytes.data(), b.blocks, pcm.data()) != FMRX_OK) {
+        const int i = filled_q.pop();
+        Slot& s = slots[i];
+        if (s.blocks > 0) {
+            CLI_HIP(hipMemcpyAsync(s.d_in, s.h_in, s.blocks * geo.block_bytes, hipMemcpyHostToDevice, up));
+            CLI_HIP(hipEventRecord(s.uploaded, up));
+            CLI_HIP(hipStreamWaitEvent(compute, s.uploaded, 0));
+            if (fmrx_process_device(ctx, s.d_in, s.blocks, s.d_out) != FMRX_OK) {
                 std::fprintf(stderr, "fmrx: %s\n", fmrx_last_error());
-                rc = 1;
-                break;
+                std::fflush(stdout);
+                std::_Exit(1);
             }
-            std::fwrite(pcm.data(), sizeof(int16_t), pcm.size(), stdout);
+            CLI_HIP(hipEventRecord(s.computed, compute));
+            CLI_HIP(hipStreamWaitEvent(down, s.computed, 0));
+            CLI_HIP(hipMemcpyAsync(s.h_out, s.d_out, s.blocks * geo.pcm_samples * sizeof(int16_t),
+                                   hipMemcpyDeviceToHost, down));
+            CLI_HIP(hipEventRecord(s.downloaded, down));
         }
-        if (b.last) break;
-    }
-    std::fflush(stdout);
-    if (rc) {
-        reader.detach();
-        fmrx_destroy(ctx);
-        std::_Exit(rc);
+        done_q.push(i);
+        if (s.last) break;
     }
     reader.join();
+    writer.join();
+    std::fflush(stdout);
+    for (Slot& s : slots) {
+        (void)hipHostFree(s.h_in);
+        (void)hipHostFree(s.h_out);
+        (void)hipFree(s.d_in);
+        (void)hipFree(s.d_out);
+        (void)hipEventDestroy(s.uploaded);
+        (void)hipEventDestroy(s.computed);
+        (void)hipEventDestroy(s.downloaded);
+    }
+    (void)hipStreamDestroy(up);
+    (void)hipStreamDestroy(down);
     fmrx_destroy(ctx);
     std::fprintf(stderr, "End of input stream reached!\n");
     return 0;

@@ -103,7 +103,11 @@ __device__ inline float sbyte(uint32_t w) {
 // lane then owns two outputs, m and m + NB, accumulated together in packed f32 ops, which
 // halves the audio stage's instructions; the neighbour I/Q for the demod comes by lane
 // shuffle instead of LDS, which pays for the larger demod window.
-template <int T, int D, int AD, int NT, int R, int PD, int ABL = 0, int PF = 1, int TR = 0, int AK = 1>
+// DB1 = 1 single-buffers the demod window (its 50-sample history is copied forward after
+// the audio stage) to save LDS for a third workgroup per SIMD.  Single-wave workgroups
+// (NT = 64) take the demod's neighbour I/Q by lane shuffle, multi-wave ones through LDS.
+template <int T, int D, int AD, int NT, int R, int PD, int ABL = 0, int PF = 1, int TR = 0, int AK = 1,
+          int DB1 = 0>
 __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps taps) {
     using C = MonoCfg<T, D, AD, NT, R>;
     constexpr int CIF = C::CIF, P = C::P, H = C::H, S = C::S, G = C::G, NLD = C::NLD;
@@ -111,10 +115,12 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     static_assert(AK == 1 || (AK == 2 && NT == 64 && CIF >= kAH), "grouped audio: one wave, CIF >= 50");
     constexpr int NB = ((2 * CIF + AD - 1) / AD + 1) / 2;  // AK = 2: output pairs per group
     static_assert(AK == 1 || NB <= NT, "one output pair per lane");
+    static_assert(DB1 == 0 || (AK == 1 && NT == 64), "single demod buffer: one wave, per-chunk audio");
+    constexpr bool kShfl = NT == 64;
 
     __shared__ float4 xb4[C::XB / 2 + 1];        // scaled (I,Q) pairs, two per float4
-    __shared__ float dbuf[2][kAH + AK * CIF];    // demod window: 50 history + AK chunks
-    __shared__ float2v pbuf[AK == 1 ? 2 : 1][AK == 1 ? NT + 1 : 1];  // last RF output per thread
+    __shared__ float dbuf[DB1 ? 1 : 2][kAH + AK * CIF];  // demod window: 50 history + AK chunks
+    __shared__ float2v pbuf[kShfl ? 1 : 2][kShfl ? 1 : NT + 1];  // last RF output per thread
     __shared__ float2 ctab2[NG + 1];             // (c[2j-1], c[2j]); c[-1] = 0
     __shared__ float atab[kAudioTaps + 1];       // audio taps
     float* ctab = reinterpret_cast<float*>(ctab2);
@@ -282,14 +288,14 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
             asm volatile("" ::"v"(acc[r]));
             acc[r] = acc[r] * 0.0078125f;  // undo the 2^7 sample scaling (exact)
         }
-        if constexpr (AK == 1) pbuf[cur][tid + 1] = acc[R - 1];
+        if constexpr (!kShfl) pbuf[cur][tid + 1] = acc[R - 1];
         __syncthreads();  // (B) all RF reads of xb done, pbuf visible
 
         // ---- carries for chunk c+1: RF history (pairs [P, P+H) -> [0, H)) as aligned 16-B
         // pair groups (P and H are even, so groups never straddle a pad), last I/Q
         for (int i = tid; i < H / 2; i += NT) xb4[C::slot(2 * i) / 2] = xb4[C::slot(P + 2 * i) / 2];
         float2v prev;
-        if constexpr (AK == 1) {
+        if constexpr (!kShfl) {
             if (tid == 0) pbuf[cur ^ 1][0] = pbuf[cur][NT];
             prev = pbuf[cur][tid];  // FM demod's previous I/Q: neighbouring thread / chunk
         } else {
@@ -315,8 +321,8 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const int jl = R * tid + r;
-            dbuf[cur][kAH + q * CIF + jl] = d[r];
-            if ((AK == 1 || q == 1) && jl >= CIF - kAH) dbuf[cur ^ 1][jl - (CIF - kAH)] = d[r];
+            dbuf[DB1 ? 0 : cur][kAH + q * CIF + jl] = d[r];
+            if (!DB1 && (AK == 1 || q == 1) && jl >= CIF - kAH) dbuf[DB1 ? 0 : cur ^ 1][jl - (CIF - kAH)] = d[r];
         }
         // Demod to global only for the split API / the chunk holding the stream's last 50
         // samples (one scalar test per chunk; the fused mono path skips it otherwise).
@@ -376,7 +382,7 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
             const long long left = n_audio - m0;  // outputs of the stream not yet written
             if (tid < C::CAmax && off0 + AD * tid < CIF && tid < left) {
                 const long long m = m0 + tid;
-                const float* dw = &dbuf[cur][off0 + AD * tid + kAH];
+                const float* dw = &dbuf[DB1 ? 0 : cur][off0 + AD * tid + kAH];
                 float a = 0.0f;
 #pragma unroll
                 for (int k = 0; k < ((ABL & 2) != 0 ? 1 : kAudioTaps); k++) {
@@ -386,6 +392,14 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                 const size_t oi = (size_t)stream * (size_t)n_audio + (size_t)m;
                 L.pcm[oi] = quantize_s16(a);
                 if (L.mono) L.mono[oi] = a;
+            }
+        }
+        if constexpr (DB1 != 0) {
+            // history for chunk c+1; one wave: its LDS operations complete in issue order,
+            // so these writes land after the audio reads above
+            if (tid < kAH) {
+                const float h = dbuf[0][CIF + tid];
+                dbuf[0][tid] = h;
             }
         }
         if constexpr (AK == 1) cur ^= 1;
@@ -619,10 +633,10 @@ int launch_wave(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStr
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-template <int T, int D, int AD, int NT, int R, int PD, int PF = 1, int TR = 0, int AK = 1>
+template <int T, int D, int AD, int NT, int R, int PD, int PF = 1, int TR = 0, int AK = 1, int DB1 = 0>
 int launch_variant(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStream_t s) {
     const dim3 grid(n_streams * L.segs), block(NT);
-    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD, 0, PF, TR, AK>), grid, block, 0, s, L, taps);
+    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD, 0, PF, TR, AK, DB1>), grid, block, 0, s, L, taps);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -634,7 +648,8 @@ struct Variant {
 constexpr Variant kVariants[] = {{256, 3, 3, 2}, {128, 3, 3, 4}, {64, 3, 3, 8}, {128, 5, 3, 3},
                                  {256, 3, 5, 2}, {64, 3, 3, 8}, {64, 3, 3, 8}, {128, 3, 3, 4},
                                  {64, 3, 3, 8}, {64, 3, 4, 8},  // 8, 9: taps in VGPRs
-                                 {64, 3, 4, 8}, {64, 3, 4, 8}};  // 10: + paired audio; 11: paired audio
+                                 {64, 3, 4, 8}, {64, 3, 4, 8},  // 10: + paired audio; 11: paired audio
+                                 {64, 2, 4, 12}, {64, 2, 3, 12}};  // 12, 13: R=2, 3 waves/SIMD
 // 5: mono_wave_kernel; 6, 7: input prefetched two chunks ahead
 constexpr int kDefaultVariant = 9;  // 64-thread workgroups (waves never wait on each other), taps in VGPRs
 
@@ -722,7 +737,11 @@ int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_de
     if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 10) \
         return launch_variant<T_, D_, AD_, 64, 3, 4, 1, 1, 2>(L, n_streams, taps, s); \
     if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 11) \
-        return launch_variant<T_, D_, AD_, 64, 3, 4, 1, 0, 2>(L, n_streams, taps, s);
+        return launch_variant<T_, D_, AD_, 64, 3, 4, 1, 0, 2>(L, n_streams, taps, s); \
+    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 12) \
+        return launch_variant<T_, D_, AD_, 64, 2, 4, 1, 0, 1, 1>(L, n_streams, taps, s); \
+    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 13) \
+        return launch_variant<T_, D_, AD_, 64, 2, 3, 1, 0, 1, 1>(L, n_streams, taps, s);
     FMRX_ALL(51, 10, 5)    // mode 0 (and mode 2's RF stage), reference taps
     FMRX_ALL(101, 10, 5)   // mode 0, 101-tap RF (BASELINE configs[1])
     FMRX_ALL(51, 4, 6)     // mode 1

@@ -319,3 +319,19 @@ def test_cli_stdin_to_stdout(fmrx, orc, mode, channels, batch):
     got = np.frombuffer(r.stdout, np.int16)
     want = orc.run(mode, 51, iq, ["pcm", "pcm_mono"])["pcm" if channels == 2 else "pcm_mono"]
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("nbytes", [0, 12799, 12800])
+def test_cli_empty_and_short_input(fmrx, orc, nbytes):
+    import os
+    import subprocess
+
+    iq = iqgen.make("rand:3", nbytes, 2400000)
+    exe = os.path.join(os.path.dirname(fmrx.LIB_PATH), "bin", "fmrx")
+    r = subprocess.run([exe, "0", "2", "--batch", "4"], input=iq.tobytes(), capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()
+    got = np.frombuffer(r.stdout, np.int16)
+    if nbytes < 12800:
+        assert got.size == 0
+    else:
+        assert np.array_equal(got, orc.run(0, 51, iq, ["pcm"])["pcm"])
