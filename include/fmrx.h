@@ -19,6 +19,8 @@
  *   fmrx_audio_block           <- audio_thread body    src/project.cpp:132-195
  *   fmrx_process               <- both bodies fused (host buffers in, host PCM out)
  *   fmrx_process_device        <- both bodies fused, device-resident buffers, async
+ *   fmrx_rds_block / _device   <- rds_thread body      src/project.cpp:200-271 (RDS front half;
+ *                                 never launched by the reference, :380-382)
  *
  * Buffers: functions named *_device / fmrx_resample etc. take DEVICE pointers and enqueue on
  * the context's HIP stream; fmrx_rf_block / fmrx_audio_block / fmrx_process take HOST
@@ -122,6 +124,19 @@ int fmrx_lr_extraction(fmrx_ctx* ctx, float* d_left, float* d_right, const float
 int fmrx_normalize_iq(fmrx_ctx* ctx, const uint8_t* d_iq, size_t n_pairs, float* d_i, float* d_q);
 /* S16 quantiser of project.cpp:185-191 (NaN -> 0, x86 truncation + 16-bit wrap).           */
 int fmrx_quantize(fmrx_ctx* ctx, const float* d_x, size_t n, int16_t* d_out);
+
+/* ---- RDS front half (rds_thread body, src/project.cpp:200-271) ------------------------- */
+/* demod (IF rate, as fmrx_rf_block returns it) -> BPF 54-60 kHz -> square -> BPF
+ * 113.5-114.5 kHz -> PLL(114 kHz, bp_fs, ncoScale 0.5, 0, 0.01) -> 5-sample channel delay ->
+ * mixer.  Every buffer is n_streams x (n_blocks * if_samples) float; rds is the mixer output
+ * (project.cpp:271 mixer_data), nco the PLL output (:259), channel the 54-60 kHz band (:247);
+ * nco and channel may be NULL.  The RDS state (filter histories, PLL, delay line) lives in the
+ * context, starts as the reference's (:206-226), is cleared by fmrx_reset and is not part of
+ * the fmrx_get_state blob.  Block-size invariant: any n_blocks per call.                     */
+int fmrx_rds_block(fmrx_ctx* ctx, const float* demod, size_t n_blocks, float* rds, float* nco,
+                   float* channel);
+int fmrx_rds_device(fmrx_ctx* ctx, const float* d_demod, size_t n_blocks, float* d_rds,
+                    float* d_nco, float* d_channel);
 
 /* ---- deterministic synthetic FM-stereo IQ; identical bytes host/device ---- */
 /* Stream `seed`, samples [first_pair, first_pair+n_pairs) of a stream at rf_fs.            */

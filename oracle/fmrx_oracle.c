@@ -277,3 +277,41 @@ long orc_run(int mode, int rf_taps, const uint8_t* iq, size_t nbytes, orc_output
     free(st_au); free(st_in);
     return n_blocks;
 }
+
+/* RDS front half, the rds_thread body (src/project.cpp:200-271, dead code in the reference):
+ * per demod block BPF 54-60 kHz (:211, :247) -> square (:250-254) -> BPF 113.5-114.5 kHz
+ * (:217, :257) -> PLL(114 kHz, bp_fs, 0.5, 0, 0.01) (:259) -> 5-sample channel delay
+ * (:262-268, rds_delay :309) -> mixer(carrier, delayed channel) (:271).  Outputs (optional,
+ * if_samples per block): channel, carrier (PLL input), nco (PLL output), rds (mixer). */
+long orc_rds(int mode, const float* demod, size_t n_blocks, float* channel, float* carrier,
+             float* nco, float* rds) {
+    orc_mode m;
+    if (orc_geometry(mode, &m) != 0) return -1;
+    enum { T = 51, DLY = 5 };
+    const int NIF = m.if_samples;
+    float ex_c[T], ca_c[T], st_ex[T - 1], st_ca[T - 1], shift_st[DLY], pll[6] = {0, 0, 1, 0, 1, 0};
+    orc_bpf(ex_c, (float)m.bp_fs, 54000.0f, 60000.0f, T);
+    orc_bpf(ca_c, (float)m.bp_fs, 113500.0f, 114500.0f, T);
+    memset(st_ex, 0, sizeof st_ex);
+    memset(st_ca, 0, sizeof st_ca);
+    memset(shift_st, 0, sizeof shift_st);
+    float* ch = (float*)malloc(sizeof(float) * NIF);
+    float* sq = (float*)malloc(sizeof(float) * NIF);
+    float* ca = (float*)malloc(sizeof(float) * NIF);
+    float* sh = (float*)malloc(sizeof(float) * NIF);
+    for (size_t b = 0; b < n_blocks; b++) {
+        orc_resample(ch, st_ex, demod + b * NIF, NIF, ex_c, T, 1, 1);
+        for (int i = 0; i < NIF; i++) sq[i] = ch[i] * ch[i];
+        orc_resample(ca, st_ca, sq, NIF, ca_c, T, 1, 1);
+        if (carrier) memcpy(carrier + b * NIF, ca, sizeof(float) * NIF);
+        orc_pll(ca, NIF, 114000.0f, (float)m.bp_fs, 0.5f, 0.0f, 0.01f, pll);
+        memcpy(sh, shift_st, sizeof shift_st);
+        memcpy(sh + DLY, ch, sizeof(float) * (NIF - DLY));
+        memcpy(shift_st, ch + NIF - DLY, sizeof shift_st);
+        if (channel) memcpy(channel + b * NIF, ch, sizeof(float) * NIF);
+        if (nco) memcpy(nco + b * NIF, ca, sizeof(float) * NIF);
+        if (rds) orc_mixer(rds + b * NIF, ca, sh, NIF);
+    }
+    free(ch); free(sq); free(ca); free(sh);
+    return (long)n_blocks;
+}

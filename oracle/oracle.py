@@ -148,6 +148,21 @@ class _Lib:
         f(_ptr(io, _fp), io.size, freq, fs, nco_scale, phase_adjust, norm_bw, _ptr(st, _fp))
         return io, st
 
+    def rds(self, mode: int, demod) -> dict:
+        """RDS front half (project.cpp:200-271) over whole demod blocks: channel, carrier (PLL
+        input), nco (PLL output) and rds (mixer output), if_samples per block each."""
+        demod = np.ascontiguousarray(demod, np.float32)
+        nif = MODES[mode][1]
+        nb = demod.size // nif
+        out = {k: np.zeros(nb * nif, np.float32) for k in ("channel", "carrier", "nco", "rds")}
+        f = getattr(self.lib, self.prefix + "rds")
+        f.restype = C.c_long
+        f.argtypes = [C.c_int, _fp, C.c_size_t, _fp, _fp, _fp, _fp]
+        n = f(mode, _ptr(demod, _fp), nb, *(_ptr(out[k], _fp) for k in ("channel", "carrier", "nco", "rds")))
+        if n < 0:
+            raise ValueError("bad mode")
+        return out
+
     def normalize(self, b):
         b = _as_u8(b)
         out = np.zeros(b.size, np.float32)

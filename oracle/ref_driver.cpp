@@ -299,4 +299,47 @@ long ref_run_mono(int mode, int rf_taps, const uint8_t* iq, size_t nbytes, int16
     return n_blocks;
 }
 
+// RDS front half, rds_thread body (src/project.cpp:200-271; dead code in the reference: the
+// thread launch is commented out at :380-382, its constants at :308-309): per demod block
+//   resample(channel, BPF 54-60 kHz) -> square -> resample(carrier, BPF 113.5-114.5 kHz) ->
+//   PLL(114 kHz, bp_fs, ncoScale 0.5, phaseAdjust 0, normBW 0.01) -> channel delay (5) ->
+//   mixer(carrier, delayed channel).
+// The 3 kHz LPF it designs (:229-230) is never applied and is not reproduced.  Outputs (all
+// optional, if_samples per block each): channel, carrier (before the PLL), nco (PLL output),
+// rds (mixer output).  Returns the number of blocks, -1 on a bad mode.
+long ref_rds(int mode, const float* demod, size_t n_blocks, float* channel, float* carrier,
+             float* nco, float* rds) {
+    RefMode m;
+    if (!ref_mode(mode, &m)) return -1;
+    const int bp_taps = 51, channel_delay = 5;  // project.cpp:307, :309 (rds_delay)
+    const size_t nif = (size_t)(256 * m.rf_decim * m.audio_decim) / 2 / m.rf_decim;  // IF samples/block
+    std::vector<float> channel_shift, channel_shift_state(channel_delay, 0.0f), channel_data;
+    std::vector<float> channel_state(bp_taps - 1, 0.0f), extract_coeff;
+    impulseResponseBPF(extract_coeff, m.bp_fs, 54000, 60000, bp_taps);
+    std::vector<float> channel_squared, carrier_data, carrier_state(bp_taps - 1, 0.0f), carrier_coeff;
+    impulseResponseBPF(carrier_coeff, m.bp_fs, 113500, 114500, bp_taps);
+    float integrator = 0.0f, phaseEst = 0.0f, feedbackI = 1.0f, feedbackQ = 0.0f, trigOffset = 0.0f;
+    float ncoOut_state = 1.0f;
+    std::vector<float> mixer_data;
+    for (size_t b = 0; b < n_blocks; b++) {
+        std::vector<float> demod_data(demod + b * nif, demod + (b + 1) * nif);
+        resample(channel_data, channel_state, demod_data, extract_coeff, 1, 1);
+        channel_squared.assign(channel_data.size(), 0.0f);
+        for (size_t i = 0; i < channel_data.size(); i++) channel_squared[i] = channel_data[i] * channel_data[i];
+        resample(carrier_data, carrier_state, channel_squared, carrier_coeff, 1, 1);
+        put(carrier, b * nif, carrier_data);
+        PLL(carrier_data, 114000, m.bp_fs, 0.5, 0, 0.01, integrator, phaseEst, feedbackI, feedbackQ,
+            ncoOut_state, trigOffset);
+        channel_shift.clear();
+        channel_shift.insert(channel_shift.end(), channel_shift_state.begin(), channel_shift_state.end());
+        channel_shift.insert(channel_shift.end(), channel_data.begin(), channel_data.end() - channel_delay);
+        channel_shift_state.assign(channel_data.end() - channel_delay, channel_data.end());
+        mixer(mixer_data, carrier_data, channel_shift);
+        put(channel, b * nif, channel_data);
+        put(nco, b * nif, carrier_data);
+        put(rds, b * nif, mixer_data);
+    }
+    return (long)n_blocks;
+}
+
 }  // extern "C"

@@ -94,6 +94,13 @@ struct fmrx_ctx {
     DevBuf<float> d_pll;          // n_streams x 8
     DevBuf<float> d_mix_tail;     // n_streams x kMixTail
     DevBuf<float> d_mono_state;   // n_streams x 8
+    // RDS front half state (project.cpp:200-271; not part of the checkpoint blob)
+    DevBuf<float> d_rds_taps;     // 54-60 kHz taps, then 113.5-114.5 kHz taps
+    DevBuf<float> d_rds_dhist;    // n_streams x kRdsDemodHist
+    DevBuf<float> d_rds_chan;     // n_streams x (kRdsChanHist + cap)
+    size_t rds_chan_stride = 0;
+    DevBuf<float> d_rds_car;      // n_streams x cap
+    DevBuf<float> d_rds_pll;      // n_streams x 8
     // staging for the host-buffer entry points
     DevBuf<uint8_t> d_in;
     DevBuf<int16_t> d_out;
@@ -155,7 +162,61 @@ int reset_state(fmrx_ctx* c) {
                           hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemsetAsync(c->d_mix_tail.p, 0, sizeof(float) * kMixTail * ns, c->stream));
     HIPCHK(hipMemsetAsync(c->d_mono_state.p, 0, sizeof(float) * 8 * ns, c->stream));
+    // RDS (project.cpp:206-226): zero histories, the same PLL start as the pilot PLL
+    HIPCHK(hipMemsetAsync(c->d_rds_dhist.p, 0, sizeof(float) * kRdsDemodHist * ns, c->stream));
+    if (c->d_rds_chan.p) HIPCHK(hipMemsetAsync(c->d_rds_chan.p, 0, sizeof(float) * c->d_rds_chan.n, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_rds_pll.p, pll.data(), sizeof(float) * pll.size(), hipMemcpyHostToDevice,
+                          c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// RDS front half over n_if new demod samples per stream (d_demod: ns x n_if, stride
+// demod_stride).  Optional copies of the NCO and the channel (ns x n_if each).
+int run_rds(fmrx_ctx* c, const float* d_demod, size_t demod_stride, size_t n_if, float* d_out,
+            float* d_nco, float* d_channel) {
+    const int ns = c->cfg.n_streams;
+    if (kRdsChanHist + n_if > c->rds_chan_stride) {
+        const size_t stride = kRdsChanHist + n_if;
+        DevBuf<float> nb;
+        int rc = nb.ensure(stride * ns);
+        if (rc) return rc;
+        HIPCHK(hipMemsetAsync(nb.p, 0, sizeof(float) * nb.n, c->stream));
+        if (c->d_rds_chan.p) {
+            HIPCHK(hipMemcpy2DAsync(nb.p, stride * sizeof(float), c->d_rds_chan.p,
+                                    c->rds_chan_stride * sizeof(float), kRdsChanHist * sizeof(float), ns,
+                                    hipMemcpyDeviceToDevice, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            c->d_rds_chan.release();
+        }
+        c->d_rds_chan = nb;
+        c->rds_chan_stride = stride;
+    }
+    int rc = c->d_rds_car.ensure(n_if * ns);
+    if (rc) return rc;
+    RdsLaunch L{};
+    L.demod = d_demod;
+    L.demod_stride = demod_stride;
+    L.dhist = c->d_rds_dhist.p;
+    L.chan = c->d_rds_chan.p;
+    L.chan_stride = c->rds_chan_stride;
+    L.carrier = c->d_rds_car.p;
+    L.car_stride = n_if;
+    L.out = d_out;
+    L.out_stride = n_if;
+    L.pll = c->d_rds_pll.p;
+    L.ex = c->d_rds_taps.p;
+    L.ca = c->d_rds_taps.p + kRdsTaps;
+    L.bp_fs = (float)c->geo.bp_fs;
+    L.n_if = (int)n_if;
+    if (launch_rds(L, ns, c->stream)) return fail(FMRX_EHIP, "RDS launch failed");
+    if (d_nco)
+        HIPCHK(hipMemcpyAsync(d_nco, c->d_rds_car.p, sizeof(float) * n_if * ns, hipMemcpyDeviceToDevice,
+                              c->stream));
+    if (d_channel)
+        HIPCHK(hipMemcpy2DAsync(d_channel, n_if * sizeof(float), c->d_rds_chan.p + kRdsChanHist,
+                                c->rds_chan_stride * sizeof(float), n_if * sizeof(float), ns,
+                                hipMemcpyDeviceToDevice, c->stream));
     return 0;
 }
 
@@ -403,8 +464,16 @@ int fmrx_create(const fmrx_config* cfg, fmrx_ctx** out) {
         (rc = c->d_audio_hist.ensure((size_t)c->audio_hist * ns)) ||
         (rc = c->d_audio.ensure(c->audio.size())) || (rc = c->d_rf.ensure(c->rf.size())) ||
         (rc = c->d_pll.ensure(8 * (size_t)ns)) || (rc = c->d_mix_tail.ensure((size_t)kMixTail * ns)) ||
-        (rc = c->d_mono_state.ensure(8 * (size_t)ns)) || (rc = c->d_sintab.ensure(kSinSize)))
+        (rc = c->d_mono_state.ensure(8 * (size_t)ns)) || (rc = c->d_sintab.ensure(kSinSize)) ||
+        (rc = c->d_rds_taps.ensure(2 * kRdsTaps)) || (rc = c->d_rds_dhist.ensure((size_t)kRdsDemodHist * ns)) ||
+        (rc = c->d_rds_pll.ensure(8 * (size_t)ns)))
         return cleanup(rc);
+    // RDS taps, project.cpp:211 and :217 (bp_taps = 51 at bp_fs)
+    std::vector<float> rds_taps(2 * kRdsTaps);
+    design_bpf(rds_taps.data(), (float)g.bp_fs, 54000.0f, 60000.0f, kRdsTaps);
+    design_bpf(rds_taps.data() + kRdsTaps, (float)g.bp_fs, 113500.0f, 114500.0f, kRdsTaps);
+    if (hipMemcpy(c->d_rds_taps.p, rds_taps.data(), sizeof(float) * rds_taps.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return cleanup(fail(FMRX_EHIP, "RDS tap upload failed"));
     if (hipMemcpy(c->d_audio.p, c->audio.data(), sizeof(float) * c->audio.size(), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_rf.p, c->rf.data(), sizeof(float) * c->rf.size(), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_sintab.p, synth_sintab(), sizeof(int16_t) * kSinSize, hipMemcpyHostToDevice) != hipSuccess)
@@ -422,6 +491,8 @@ void fmrx_destroy(fmrx_ctx* c) {
     c->d_audio_hist.release(); c->d_demod.release(); c->d_channel.release(); c->d_carrier.release();
     c->d_pll.release(); c->d_mix_tail.release(); c->d_mono_state.release(); c->d_in.release();
     c->d_out.release(); c->d_f32.release(); c->d_scratch.release(); c->d_sintab.release();
+    c->d_rds_taps.release(); c->d_rds_dhist.release(); c->d_rds_chan.release(); c->d_rds_car.release();
+    c->d_rds_pll.release();
     for (auto& e : c->evs) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
@@ -623,6 +694,40 @@ int fmrx_audio_block(fmrx_ctx* c, const float* demod, size_t n_blocks, int16_t* 
     HIPCHK(hipMemcpyAsync(pcm, c->d_out.p, out_n * sizeof(int16_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return FMRX_OK;
+}
+
+// ---- RDS front half (rds_thread body, project.cpp:200-271) -------------------------------
+int fmrx_rds_block(fmrx_ctx* c, const float* demod, size_t n_blocks, float* rds, float* nco,
+                   float* channel) {
+    CtxLock lock_(c);
+    if (!c || !demod || !rds) return fail(FMRX_EINVAL, "null argument");
+    if (n_blocks == 0) return FMRX_OK;
+    int rc = set_device(c);
+    if (rc) return rc;
+    const size_t ns = c->cfg.n_streams;
+    const size_t n = ns * n_blocks * c->geo.if_samples;
+    if ((rc = c->d_f32.ensure(n)) || (rc = c->d_scratch.ensure(3 * n))) return rc;
+    float* d_rds = c->d_scratch.p;
+    float* d_nco = nco ? c->d_scratch.p + n : nullptr;
+    float* d_ch = channel ? c->d_scratch.p + 2 * n : nullptr;
+    HIPCHK(hipMemcpyAsync(c->d_f32.p, demod, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+    if ((rc = run_rds(c, c->d_f32.p, n / ns, n / ns, d_rds, d_nco, d_ch))) return rc;
+    HIPCHK(hipMemcpyAsync(rds, d_rds, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+    if (nco) HIPCHK(hipMemcpyAsync(nco, d_nco, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+    if (channel) HIPCHK(hipMemcpyAsync(channel, d_ch, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return FMRX_OK;
+}
+
+int fmrx_rds_device(fmrx_ctx* c, const float* d_demod, size_t n_blocks, float* d_rds, float* d_nco,
+                    float* d_channel) {
+    CtxLock lock_(c);
+    if (!c || !d_demod || !d_rds) return fail(FMRX_EINVAL, "null argument");
+    if (n_blocks == 0) return FMRX_OK;
+    int rc = set_device(c);
+    if (rc) return rc;
+    const size_t n_if = n_blocks * c->geo.if_samples;
+    return run_rds(c, d_demod, n_if, n_if, d_rds, d_nco, d_channel);
 }
 
 // ---- filter.h primitives ---------------------------------------------------------------

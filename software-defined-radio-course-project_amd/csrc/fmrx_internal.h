@@ -93,6 +93,29 @@ struct AudioLaunch {
 };
 int launch_stereo_audio(const AudioLaunch& L, int n_streams, hipStream_t s);
 
+// ---- RDS front half (project.cpp:200-271) ----------------------------------------------
+constexpr int kRdsTaps = 51;        // bp_taps, project.cpp:307
+constexpr int kRdsDelay = 5;        // rds_delay, project.cpp:309 (commented constant)
+constexpr int kRdsDemodHist = 2 * (kRdsTaps - 1);  // both FIRs' history, in demod samples
+constexpr int kRdsChanHist = 8;     // >= kRdsDelay channel samples kept in front
+struct RdsLaunch {
+    const float* demod;     // n_streams x n_if (stride demod_stride), the call's demod
+    size_t demod_stride;
+    float* dhist;           // n_streams x kRdsDemodHist: demod samples before this call
+    float* chan;            // n_streams x (kRdsChanHist + n_if): channel, its tail in front
+    size_t chan_stride;
+    float* carrier;         // n_streams x n_if: BPF output, then (PLL in place) the NCO
+    size_t car_stride;
+    float* out;             // n_streams x n_if: mixer output
+    size_t out_stride;
+    float* pll;             // n_streams x 8 PLL state
+    const float* ex;        // 54-60 kHz taps (device)
+    const float* ca;        // 113.5-114.5 kHz taps (device)
+    float bp_fs;
+    int n_if;
+};
+int launch_rds(const RdsLaunch& L, int n_streams, hipStream_t s);
+
 // ---- generic filter.h primitives ------------------------------------------------------
 int launch_resample(float* out, const float* state, const float* in, int n_in,
                     const float* coeff, int taps, int up, int down, int n_out, hipStream_t s);

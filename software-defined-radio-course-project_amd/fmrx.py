@@ -59,6 +59,8 @@ PROTOTYPES = {
     "fmrx_process": (C.c_int, [_vp, _vp, _sz, _vp]),
     "fmrx_rf_block": (C.c_int, [_vp, _vp, _sz, _vp]),
     "fmrx_audio_block": (C.c_int, [_vp, _vp, _sz, _vp]),
+    "fmrx_rds_block": (C.c_int, [_vp, _vp, _sz, _vp, _vp, _vp]),
+    "fmrx_rds_device": (C.c_int, [_vp, _vp, _sz, _vp, _vp, _vp]),
     "fmrx_process_device": (C.c_int, [_vp, _vp, _sz, _vp]),
     "fmrx_process_device_ex": (C.c_int, [_vp, _vp, _sz, _vp, _vp]),
     "fmrx_synchronize": (C.c_int, [_vp]),
@@ -219,6 +221,28 @@ class Receiver:
         if nb:
             _check(lib().fmrx_audio_block(self.h, _np_ptr(d), nb, _np_ptr(out)))
         return out if self.n_streams > 1 else out[0]
+
+    def rds_block(self, demod: np.ndarray, want_nco: bool = False, want_channel: bool = False):
+        """rds_thread body (project.cpp:200-271): demod floats -> RDS mixer output (and
+        optionally the PLL output and the 54-60 kHz channel).  Returns a dict of arrays."""
+        d = np.ascontiguousarray(demod, np.float32).reshape(self.n_streams, -1)
+        nb = d.shape[1] // self.geo.if_samples
+        n = nb * self.geo.if_samples
+        d = np.ascontiguousarray(d[:, :n])
+        out = {"rds": np.zeros((self.n_streams, n), np.float32)}
+        if want_nco:
+            out["nco"] = np.zeros((self.n_streams, n), np.float32)
+        if want_channel:
+            out["channel"] = np.zeros((self.n_streams, n), np.float32)
+        if nb:
+            _check(lib().fmrx_rds_block(self.h, _np_ptr(d), nb, _np_ptr(out["rds"]),
+                                        _np_ptr(out["nco"]) if want_nco else None,
+                                        _np_ptr(out["channel"]) if want_channel else None))
+        return {k: (v if self.n_streams > 1 else v[0]) for k, v in out.items()}
+
+    def rds_device(self, d_demod: int, n_blocks: int, d_rds: int, d_nco: int | None = None,
+                   d_channel: int | None = None) -> None:
+        _check(lib().fmrx_rds_device(self.h, d_demod, n_blocks, d_rds, d_nco, d_channel))
 
     # ---- device entry points (pointers are device addresses)
     def process_device(self, d_iq: int, n_blocks: int, d_pcm: int, d_mono: int | None = None) -> None:

@@ -94,3 +94,36 @@ def has_gpu() -> bool:
         return torch.cuda.is_available()
     except Exception:
         return False
+
+
+# ---- RDS front half fixtures (tests/golden/rds_*.npz) ------------------------------------
+
+def rds_cases():
+    return sorted(os.path.basename(p)[4:-4] for p in glob.glob(os.path.join(GOLDEN, "rds_*.npz")))
+
+
+def load_rds(name):
+    z = dict(np.load(os.path.join(GOLDEN, f"rds_{name}.npz")))
+    for k in ("mode", "n_blocks"):
+        z[k] = int(z[k])
+    for k in list(z):
+        if k == "source" or k.endswith("_sha256"):
+            z[k] = str(z[k])
+    return z
+
+
+def rds_input(orc, z):
+    """The demod input of an RDS fixture: stored (rds57:) or the pinned oracle front end on
+    the I/Q recipe (iq:), checked against the stored SHA-256 either way."""
+    import hashlib
+
+    import oracle
+
+    if "demod" in z:
+        demod = z["demod"]
+    else:
+        bb, rf_fs = oracle.MODES[z["mode"]][0], oracle.MODES[z["mode"]][3]
+        iq = iqgen.make(z["source"][3:], z["n_blocks"] * bb, rf_fs)
+        demod = orc.run(z["mode"], 51, iq, ["demod"])["demod"]
+    assert hashlib.sha256(np.ascontiguousarray(demod).tobytes()).hexdigest() == z["demod_sha256"]
+    return demod

@@ -62,3 +62,23 @@ def make(recipe: str, n_bytes: int, rf_fs: int = 2400000) -> np.ndarray:
 
 def bytes_(recipe: str, n: int) -> np.ndarray:
     return make(recipe, n)
+
+
+def make_rds_demod(seed: int, n: int, fs: int) -> np.ndarray:
+    """A demod-rate (IF) test signal for the RDS front half: 1 kHz mono tone, 19 kHz pilot
+    and a 57 kHz subcarrier carrying biphase-coded random bits at 1187.5 bit/s, plus a little
+    noise.  Computed in float64, stored as float32; fixtures keep the array itself (the tests
+    never regenerate it), so libm differences between machines cannot matter."""
+    t = np.arange(n, dtype=np.float64) / fs
+    nbits = int(n / fs * 1187.5) + 2
+    idx = np.arange(nbits, dtype=np.uint64) + (np.uint64(seed) << np.uint64(40))
+    bits = (splitmix64(idx) >> np.uint64(63)).astype(np.float64)
+    sym = 2.0 * bits - 1.0
+    ph = t * 1187.5
+    k = np.floor(ph).astype(np.int64)
+    half = np.where(ph - k < 0.5, 1.0, -1.0)  # biphase (Manchester) symbol shape
+    rds = sym[k] * half
+    noise = (rand_bytes(seed + 17, n).astype(np.float64) - 127.5) / 127.5
+    x = (0.30 * np.sin(2 * np.pi * 1000.0 * t) + 0.05 * np.cos(2 * np.pi * 19000.0 * t)
+         + 0.04 * rds * np.cos(2 * np.pi * 57000.0 * t) + 0.002 * noise)
+    return x.astype(np.float32)

@@ -335,3 +335,59 @@ def test_cli_empty_and_short_input(fmrx, orc, nbytes):
         assert got.size == 0
     else:
         assert np.array_equal(got, orc.run(0, 51, iq, ["pcm"])["pcm"])
+
+
+# ---- RDS front half (rds_thread body, project.cpp:200-271) -----------------------------------
+
+from conftest import load_rds, rds_cases, rds_input  # noqa: E402
+
+
+@pytest.mark.parametrize("name", rds_cases())
+def test_rds_matches_reference(fmrx, orc, name):
+    z = load_rds(name)
+    demod = rds_input(orc, z)
+    with fmrx.Receiver(z["mode"], fmrx.STEREO) as rx:
+        out = rx.rds_block(demod, want_nco=True, want_channel=True)
+    for f in ("channel", "nco", "rds"):
+        if f in z:
+            assert same(out[f], z[f]), f
+        assert sha(out[f]) == z[f + "_sha256"], f
+
+
+def test_rds_call_split_and_reset(fmrx, orc):
+    z = load_rds("m0_rds57")
+    demod, nif = z["demod"], oracle.MODES[0][1]
+    with fmrx.Receiver(0, fmrx.MONO) as rx:
+        parts, b = [], 0
+        for nb in (1, 5, 2, 16):
+            parts.append(rx.rds_block(demod[b * nif:(b + nb) * nif])["rds"])
+            b += nb
+        assert same(np.concatenate(parts), z["rds"])
+        rx.reset()
+        assert same(rx.rds_block(demod)["rds"], z["rds"])
+
+
+def test_rds_multistream_and_device_api(fmrx, orc):
+    nif, nb = oracle.MODES[1][1], 10
+    ins = [iqgen.make_rds_demod(60 + s, nb * nif, oracle.MODES[1][5]) for s in range(3)]
+    ins[2] = ins[2] * np.float32(-2.5)
+    want = [orc.rds(1, x) for x in ins]
+    with fmrx.Receiver(1, fmrx.STEREO, n_streams=3) as rx:
+        got = rx.rds_block(np.stack(ins), want_nco=True, want_channel=True)
+    for s in range(3):
+        for f in ("rds", "nco", "channel"):
+            assert same(got[f][s], want[s][f]), (s, f)
+    # device entry point: n_streams x (n_blocks * if_samples) contiguous, two calls of halves
+    with fmrx.Receiver(1, fmrx.STEREO, n_streams=3) as rx:
+        half = nb // 2 * nif
+        outs = []
+        for h in range(2):
+            d_in = torch.from_numpy(np.stack([x[h * half:(h + 1) * half] for x in ins])).cuda()
+            d_out = torch.empty_like(d_in)
+            d_nco = torch.empty_like(d_in)
+            rx.rds_device(d_in.data_ptr(), nb // 2, d_out.data_ptr(), d_nco.data_ptr())
+            rx.synchronize()
+            outs.append((d_out.cpu().numpy(), d_nco.cpu().numpy()))
+    for s in range(3):
+        assert same(np.concatenate([o[0][s] for o in outs]), want[s]["rds"]), s
+        assert same(np.concatenate([o[1][s] for o in outs]), want[s]["nco"]), s

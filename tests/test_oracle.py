@@ -114,3 +114,32 @@ def test_oracle_vs_reference_live(orc, ref, mode, rf_taps, recipe, nb):
     b = ref.run(mode, rf_taps, iq)
     for f in oracle.FIELDS:
         assert np.array_equal(bits(a[f]), bits(b[f])), f
+
+
+# ---- RDS front half (project.cpp:200-271) ------------------------------------------------
+
+from conftest import load_rds, rds_cases, rds_input  # noqa: E402
+
+RDS_FIELDS = ("channel", "carrier", "nco", "rds")
+
+
+@pytest.mark.parametrize("name", rds_cases())
+def test_oracle_rds_matches_golden(orc, name):
+    z = load_rds(name)
+    if z["n_blocks"] > 100:
+        pytest.skip("long case: GPU tests compare it; the oracle pass is covered by the short ones")
+    out = orc.rds(z["mode"], rds_input(orc, z))
+    for f in RDS_FIELDS:
+        if f in z:
+            assert np.array_equal(bits(out[f]), bits(z[f])), f
+        assert sha(out[f]) == z[f + "_sha256"], f
+
+
+@pytest.mark.parametrize("mode,nb", [(0, 11), (1, 9)])
+def test_oracle_rds_vs_reference_live(orc, ref, mode, nb):
+    nif = oracle.MODES[mode][1]
+    demod = iqgen.make_rds_demod(50 + mode, nb * nif, oracle.MODES[mode][5])
+    demod[::97] *= -3.0  # impulsive samples
+    a, b = orc.rds(mode, demod), ref.rds(mode, demod)
+    for f in RDS_FIELDS:
+        assert np.array_equal(bits(a[f]), bits(b[f])), f
