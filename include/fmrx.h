@@ -21,6 +21,9 @@
  *   fmrx_process_device        <- both bodies fused, device-resident buffers, async
  *   fmrx_rds_block / _device   <- rds_thread body      src/project.cpp:200-271 (RDS front half;
  *                                 never launched by the reference, :380-382)
+ *   fmrx_fm_demod_arctan       <- fmDemodArctan        model/fmSupportLib.py:34-63
+ *   fmrx_estimate_psd          <- estimatePSD          include/fourier.h:27-31, src/fourier.cpp:35-117
+ *   fmrx_psd_device               (model/fmSupportLib.py:83-157)
  *
  * Buffers: functions named *_device / fmrx_resample etc. take DEVICE pointers and enqueue on
  * the context's HIP stream; fmrx_rf_block / fmrx_audio_block / fmrx_process take HOST
@@ -137,6 +140,22 @@ int fmrx_rds_block(fmrx_ctx* ctx, const float* demod, size_t n_blocks, float* rd
                    float* channel);
 int fmrx_rds_device(fmrx_ctx* ctx, const float* d_demod, size_t n_blocks, float* d_rds,
                     float* d_nco, float* d_channel);
+
+/* ---- arctan demodulator and PSD estimate (floating-point diagnostics) ------ */
+/* fmDemodArctan: out[k] = atan2(Q,I) phase difference to the previous sample, wrapped into
+ * [-pi, pi] as np.unwrap does; computed in double, stored as float.  d_prev_phase (one double,
+ * in/out) is the phase before d_i[0]; on return the principal phase of the last sample (the
+ * model returns the unwrapped one: equal mod 2 pi).  Device buffers, async.                  */
+int fmrx_fm_demod_arctan(fmrx_ctx* ctx, float* d_out, double* d_prev_phase, const float* d_i,
+                         const float* d_q, int n);
+/* estimatePSD: Hann window, floor(n / freq_bins) segments, 10 log10(4/(Fs N) |X|^2) for the
+ * freq_bins/2 positive bins, averaged in dB over segments.  freq_bins: power of two in
+ * [2, 8192] (FFT in double; the reference's O(N^2) float DFT allows any N); n >= freq_bins.
+ * Host buffers: freq and psd_db hold freq_bins/2 floats (freq[i] = i * fs / freq_bins).    */
+int fmrx_estimate_psd(fmrx_ctx* ctx, const float* samples, size_t n, int freq_bins, float fs,
+                      float* freq, float* psd_db);
+int fmrx_psd_device(fmrx_ctx* ctx, const float* d_samples, size_t n, int freq_bins, float fs,
+                    float* d_psd_db);
 
 /* ---- deterministic synthetic FM-stereo IQ; identical bytes host/device ---- */
 /* Stream `seed`, samples [first_pair, first_pair+n_pairs) of a stream at rf_fs.            */

@@ -315,3 +315,76 @@ long orc_rds(int mode, const float* demod, size_t n_blocks, float* channel, floa
     free(ch); free(sq); free(ca); free(sh);
     return (long)n_blocks;
 }
+
+/* fmDemodArctan (model/fmSupportLib.py:34-63), float64 like the model: per sample
+ * current_phase = atan2(Q, I); [prev, current] = np.unwrap([prev, current]); demod = current -
+ * prev; prev = current (the UNWRAPPED phase, which keeps growing).  np.unwrap (numpy 2.x):
+ * dd = cur - prev; ddmod = mod(dd + pi, 2 pi) - pi (numpy's floored mod); ddmod = pi where
+ * ddmod == -pi and dd > 0; correction ddmod - dd, zeroed when |dd| < pi. */
+static double np_mod(double x, double y) {
+    double m = fmod(x, y);
+    if (m != 0.0 && ((y < 0.0) != (m < 0.0))) m += y;
+    return m;
+}
+
+int orc_fm_demod_arctan(double* out, double* prev_phase, const double* i_in, const double* q_in, int n) {
+    const double pi = 3.141592653589793, two_pi = 2.0 * pi;
+    double prev = *prev_phase;
+    for (int k = 0; k < n; k++) {
+        const double cur = atan2(q_in[k], i_in[k]);
+        const double dd = cur - prev;
+        double ddmod = np_mod(dd + pi, two_pi) - pi;
+        if (ddmod == -pi && dd > 0.0) ddmod = pi;
+        double corr = ddmod - dd;
+        if (fabs(dd) < pi) corr = 0.0;
+        const double unwrapped = cur + corr;
+        out[k] = unwrapped - prev;
+        prev = unwrapped;
+    }
+    *prev_phase = prev;
+    return n;
+}
+
+/* estimatePSD (src/fourier.cpp:35-117; model/fmSupportLib.py:83-157) restated accurately:
+ * float Hann window sin(i pi / N)^2 (double, rounded to float, as fourier.cpp:59-61), float
+ * windowed samples, DFT in double with exact twiddle angles 2 pi (k m mod N) / N,
+ * 10 log10(4/(Fs N) |X|^2) per positive bin, float mean over segments in segment order. */
+int orc_estimate_psd(const float* samples, size_t n, int freq_bins, float fs, float* freq, float* psd) {
+    const int N = freq_bins, half = N / 2;
+    const int nseg = (int)(n / (size_t)N);
+    if (N < 2 || nseg < 1) return -1;
+    const double pi = 3.14159265358979323846;
+    const float df = fs / (float)N;
+    for (int i = 0; i < half; i++) freq[i] = (float)i * df;
+    float* hann = (float*)malloc(sizeof(float) * N);
+    float* w = (float*)malloc(sizeof(float) * N);
+    double* cs = (double*)malloc(sizeof(double) * N);
+    double* sn = (double*)malloc(sizeof(double) * N);
+    for (int i = 0; i < N; i++) {
+        const double s = sin(i * pi / N);
+        hann[i] = (float)(s * s);
+        cs[i] = cos(2.0 * pi * i / N);
+        sn[i] = -sin(2.0 * pi * i / N);
+    }
+    for (int k = 0; k < half; k++) psd[k] = 0.0f;
+    float* seg = (float*)malloc(sizeof(float) * (size_t)half * nseg);
+    for (int l = 0; l < nseg; l++) {
+        for (int i = 0; i < N; i++) w[i] = samples[(size_t)l * N + i] * hann[i];
+        for (int m = 0; m < half; m++) {
+            double re = 0.0, im = 0.0;
+            for (int k = 0; k < N; k++) {
+                const int idx = (int)(((long long)k * m) % N);
+                re += w[k] * cs[idx];
+                im += w[k] * sn[idx];
+            }
+            seg[(size_t)l * half + m] = (float)(10.0 * log10(4.0 / ((double)fs * N) * (re * re + im * im)));
+        }
+    }
+    for (int k = 0; k < half; k++) {
+        float acc = 0.0f;
+        for (int l = 0; l < nseg; l++) acc += seg[(size_t)l * half + k];
+        psd[k] = acc / (float)nseg;
+    }
+    free(hann); free(w); free(cs); free(sn); free(seg);
+    return nseg;
+}

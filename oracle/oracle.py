@@ -163,6 +163,18 @@ class _Lib:
             raise ValueError("bad mode")
         return out
 
+    def estimate_psd(self, samples, freq_bins: int, fs: float):
+        """estimatePSD (fourier.cpp:35-117): (freq, psd_db), freq_bins/2 floats each."""
+        x = np.ascontiguousarray(samples, np.float32)
+        freq = np.zeros(freq_bins // 2, np.float32)
+        psd = np.zeros(freq_bins // 2, np.float32)
+        f = getattr(self.lib, self.prefix + "estimate_psd")
+        f.restype = C.c_int
+        f.argtypes = [_fp, C.c_size_t, C.c_int, C.c_float, _fp, _fp]
+        if f(_ptr(x, _fp), x.size, freq_bins, fs, _ptr(freq, _fp), _ptr(psd, _fp)) < 0:
+            raise ValueError("need at least one segment")
+        return freq, psd
+
     def normalize(self, b):
         b = _as_u8(b)
         out = np.zeros(b.size, np.float32)
@@ -180,6 +192,18 @@ class Oracle(_Lib):
 
     def run(self, mode, rf_taps, iq, fields=None):
         return self._run(self.lib.orc_run, mode, rf_taps, iq, fields)
+
+    def fm_demod_arctan(self, i, q, prev_phase=0.0):
+        """fmDemodArctan (model/fmSupportLib.py:34-63) in float64: (demod, last phase)."""
+        i = np.ascontiguousarray(i, np.float64)
+        q = np.ascontiguousarray(q, np.float64)
+        out = np.zeros(i.size, np.float64)
+        pv = C.c_double(prev_phase)
+        _dp = C.POINTER(C.c_double)
+        f = self.lib.orc_fm_demod_arctan
+        f.argtypes = [_dp, _dp, _dp, _dp, C.c_int]
+        f(out.ctypes.data_as(_dp), C.byref(pv), i.ctypes.data_as(_dp), q.ctypes.data_as(_dp), i.size)
+        return out, pv.value
 
     def quant(self, x):
         f = self.lib.orc_quant

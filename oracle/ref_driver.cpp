@@ -29,6 +29,7 @@
 
 #include "dy4.h"
 #include "filter.h"
+#include "fourier.h"
 #include "iofunc.h"
 
 namespace {
@@ -340,6 +341,17 @@ long ref_rds(int mode, const float* demod, size_t n_blocks, float* channel, floa
         put(rds, b * nif, mixer_data);
     }
     return (long)n_blocks;
+}
+
+// estimatePSD (src/fourier.cpp:35-117): Hann window, per-segment DFT, 10 log10 of
+// 4/(Fs N) |X|^2 over the positive half, averaged in dB over the whole segments.  freq and
+// psd hold freq_bins/2 floats.  Returns the number of segments.
+int ref_estimate_psd(const float* samples, size_t n, int freq_bins, float fs, float* freq, float* psd) {
+    std::vector<float> f, p, x(samples, samples + n);
+    estimatePSD(f, p, x, freq_bins, fs);
+    std::memcpy(freq, f.data(), f.size() * sizeof(float));
+    std::memcpy(psd, p.data(), p.size() * sizeof(float));
+    return (int)(n / (size_t)freq_bins);
 }
 
 }  // extern "C"

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -728,6 +729,66 @@ int fmrx_rds_device(fmrx_ctx* c, const float* d_demod, size_t n_blocks, float* d
     if (rc) return rc;
     const size_t n_if = n_blocks * c->geo.if_samples;
     return run_rds(c, d_demod, n_if, n_if, d_rds, d_nco, d_channel);
+}
+
+// ---- arctan demodulator and PSD estimate ------------------------------
+int fmrx_fm_demod_arctan(fmrx_ctx* c, float* d_out, double* d_prev_phase, const float* d_i,
+                         const float* d_q, int n) {
+    CtxLock lock_(c);
+    if (!c || !d_out || !d_prev_phase || !d_i || !d_q || n < 0) return fail(FMRX_EINVAL, "bad argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (launch_demod_arctan(d_out, d_prev_phase, d_i, d_q, n, c->stream)) return fail(FMRX_EHIP, "launch failed");
+    return FMRX_OK;
+}
+
+namespace {
+// estimatePSD's window (fourier.cpp:57-61): pow(sin(i*PI/N), 2) in double, stored as float.
+int psd_run(fmrx_ctx* c, const float* d_x, size_t n, int freq_bins, float fs, float* d_psd) {
+    const int N = freq_bins;
+    if (N < 2 || N > kPsdMaxBins || (N & (N - 1)) != 0)
+        return fail(FMRX_EINVAL, "freq_bins must be a power of two in [2, %d]", kPsdMaxBins);
+    const size_t nseg = n / (size_t)N;
+    if (nseg < 1) return fail(FMRX_EINVAL, "need at least freq_bins samples");
+    int rc = c->d_scratch.ensure((size_t)N + nseg * (N / 2));
+    if (rc) return rc;
+    std::vector<float> hann(N);
+    for (int i = 0; i < N; i++) {
+        const double s = std::sin(i * 3.14159265358979323846 / N);  // PI, dy4.h:14
+        hann[i] = (float)(s * s);
+    }
+    HIPCHK(hipMemcpyAsync(c->d_scratch.p, hann.data(), sizeof(float) * N, hipMemcpyHostToDevice, c->stream));
+    // psd_seg = (4 / (Fs * freq_bins)) * |X|^2 (fourier.cpp:103)
+    const double scale = 4.0 / ((double)fs * (double)N);
+    if (launch_psd(d_x, (int)nseg, N, c->d_scratch.p, scale, c->d_scratch.p + N, d_psd, c->stream))
+        return fail(FMRX_EHIP, "PSD launch failed");
+    HIPCHK(hipStreamSynchronize(c->stream));  // the window lives in host memory until here
+    return 0;
+}
+}  // namespace
+
+int fmrx_psd_device(fmrx_ctx* c, const float* d_samples, size_t n, int freq_bins, float fs, float* d_psd) {
+    CtxLock lock_(c);
+    if (!c || !d_samples || !d_psd) return fail(FMRX_EINVAL, "null argument");
+    int rc = set_device(c);
+    return rc ? rc : psd_run(c, d_samples, n, freq_bins, fs, d_psd);
+}
+
+int fmrx_estimate_psd(fmrx_ctx* c, const float* samples, size_t n, int freq_bins, float fs, float* freq,
+                      float* psd) {
+    CtxLock lock_(c);
+    if (!c || !samples || !freq || !psd) return fail(FMRX_EINVAL, "null argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (freq_bins < 2) return fail(FMRX_EINVAL, "freq_bins must be >= 2");
+    const size_t used = n / (size_t)freq_bins * (size_t)freq_bins;
+    if ((rc = c->d_f32.ensure(used + (size_t)freq_bins / 2))) return rc;
+    HIPCHK(hipMemcpyAsync(c->d_f32.p, samples, sizeof(float) * used, hipMemcpyHostToDevice, c->stream));
+    if ((rc = psd_run(c, c->d_f32.p, used, freq_bins, fs, c->d_f32.p + used))) return rc;
+    HIPCHK(hipMemcpy(psd, c->d_f32.p + used, sizeof(float) * (freq_bins / 2), hipMemcpyDeviceToHost));
+    const float df = fs / (float)freq_bins;  // fourier.cpp:42-50
+    for (int i = 0; i < freq_bins / 2; i++) freq[i] = (float)i * df;
+    return FMRX_OK;
 }
 
 // ---- filter.h primitives ---------------------------------------------------------------

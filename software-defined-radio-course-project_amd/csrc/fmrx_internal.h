@@ -116,6 +116,12 @@ struct RdsLaunch {
 };
 int launch_rds(const RdsLaunch& L, int n_streams, hipStream_t s);
 
+// ---- spectrum tooling and the arctan demodulator ------------------
+constexpr int kPsdMaxBins = 8192;  // N complex doubles in LDS per segment
+int launch_demod_arctan(float* out, double* prev, const float* i, const float* q, int n, hipStream_t s);
+int launch_psd(const float* x, int nseg, int N, const float* hann, double scale, float* seg_db, float* psd,
+               hipStream_t s);
+
 // ---- generic filter.h primitives ------------------------------------------------------
 int launch_resample(float* out, const float* state, const float* in, int n_in,
                     const float* coeff, int taps, int up, int down, int n_out, hipStream_t s);

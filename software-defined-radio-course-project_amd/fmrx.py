@@ -61,6 +61,9 @@ PROTOTYPES = {
     "fmrx_audio_block": (C.c_int, [_vp, _vp, _sz, _vp]),
     "fmrx_rds_block": (C.c_int, [_vp, _vp, _sz, _vp, _vp, _vp]),
     "fmrx_rds_device": (C.c_int, [_vp, _vp, _sz, _vp, _vp, _vp]),
+    "fmrx_fm_demod_arctan": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_int]),
+    "fmrx_estimate_psd": (C.c_int, [_vp, _vp, _sz, C.c_int, C.c_float, _vp, _vp]),
+    "fmrx_psd_device": (C.c_int, [_vp, _vp, _sz, C.c_int, C.c_float, _vp]),
     "fmrx_process_device": (C.c_int, [_vp, _vp, _sz, _vp]),
     "fmrx_process_device_ex": (C.c_int, [_vp, _vp, _sz, _vp, _vp]),
     "fmrx_synchronize": (C.c_int, [_vp]),
@@ -243,6 +246,21 @@ class Receiver:
     def rds_device(self, d_demod: int, n_blocks: int, d_rds: int, d_nco: int | None = None,
                    d_channel: int | None = None) -> None:
         _check(lib().fmrx_rds_device(self.h, d_demod, n_blocks, d_rds, d_nco, d_channel))
+
+    def estimate_psd(self, samples: np.ndarray, freq_bins: int, fs: float):
+        """estimatePSD (fourier.cpp:35-117) on the GPU: (freq, psd_db)."""
+        x = np.ascontiguousarray(samples, np.float32)
+        freq = np.zeros(freq_bins // 2, np.float32)
+        psd = np.zeros(freq_bins // 2, np.float32)
+        _check(lib().fmrx_estimate_psd(self.h, _np_ptr(x), x.size, freq_bins, fs, _np_ptr(freq), _np_ptr(psd)))
+        return freq, psd
+
+    def psd_device(self, d_samples: int, n: int, freq_bins: int, fs: float, d_psd: int) -> None:
+        _check(lib().fmrx_psd_device(self.h, d_samples, n, freq_bins, fs, d_psd))
+
+    def fm_demod_arctan(self, d_out: int, d_prev_phase: int, d_i: int, d_q: int, n: int) -> None:
+        """fmDemodArctan (fmSupportLib.py:34-63) on device buffers (float in/out, double phase)."""
+        _check(lib().fmrx_fm_demod_arctan(self.h, d_out, d_prev_phase, d_i, d_q, n))
 
     # ---- device entry points (pointers are device addresses)
     def process_device(self, d_iq: int, n_blocks: int, d_pcm: int, d_mono: int | None = None) -> None:

@@ -391,3 +391,59 @@ def test_rds_multistream_and_device_api(fmrx, orc):
     for s in range(3):
         assert same(np.concatenate([o[0][s] for o in outs]), want[s]["rds"]), s
         assert same(np.concatenate([o[1][s] for o in outs]), want[s]["nco"]), s
+
+
+# ---- arctan demodulator and PSD estimate (floating point: tolerances stated) -----------------
+
+import os  # noqa: E402
+
+from test_oracle import GOLD, check_psd, psd_cases  # noqa: E402
+
+# fmDemodArctan on the GPU: double atan2 of float I/Q, wrapped, rounded to float.  Against the
+# model's float64 output the error is the final float rounding (<= 2^-24 relative) plus the
+# model's own cancellation error on its growing unwrapped phase (~1e-12 here).
+ARCTAN_RTOL = 2.0 ** -23
+ARCTAN_ATOL = 1e-9
+
+
+def test_arctan_demod_matches_python_model(fmrx):
+    z = np.load(os.path.join(GOLD, "py_arctan.npz"))
+    b = int(z["block"])
+    with fmrx.Receiver(0, fmrx.MONO) as rx:
+        prev = torch.zeros(1, dtype=torch.float64, device="cuda")
+        outs = []
+        for k in range(z["i"].size // b):
+            di = torch.from_numpy(z["i"][k * b:(k + 1) * b].copy()).cuda()
+            dq = torch.from_numpy(z["q"][k * b:(k + 1) * b].copy()).cuda()
+            do = torch.empty_like(di)
+            rx.fm_demod_arctan(do.data_ptr(), prev.data_ptr(), di.data_ptr(), dq.data_ptr(), b)
+            rx.synchronize()
+            outs.append(do.cpu().numpy())
+            # the carried phase is the principal value: equal to the model's mod 2 pi
+            dphi = float(prev.cpu()[0]) - float(z["phases"][k])
+            assert abs(dphi - 2 * np.pi * round(dphi / (2 * np.pi))) < 1e-9
+    got = np.concatenate(outs).astype(np.float64)
+    np.testing.assert_allclose(got, z["demod"], rtol=ARCTAN_RTOL, atol=ARCTAN_ATOL)
+
+
+@pytest.mark.parametrize("key", psd_cases())
+def test_psd_matches_python_model_and_cpp(fmrx, key):
+    z = np.load(os.path.join(GOLD, "py_psd.npz"))
+    name, nb, fs = key.rsplit("_", 2)
+    with fmrx.Receiver(0, fmrx.MONO) as rx:
+        freq, psd = rx.estimate_psd(z[f"x_{name}"], int(nb), float(fs))
+    check_psd(z, key, freq, psd)
+
+
+def test_psd_device_api_and_errors(fmrx, orc):
+    x = (iqgen.rand_bytes(78, 5000).astype(np.float32) - 127.5) / 127.5
+    with fmrx.Receiver(0, fmrx.MONO) as rx:
+        d_x = torch.from_numpy(x).cuda()
+        d_p = torch.empty(256, dtype=torch.float32, device="cuda")
+        rx.psd_device(d_x.data_ptr(), x.size, 512, 48000.0, d_p.data_ptr())  # 9 segments, ragged tail
+        rx.synchronize()
+        _, want = orc.estimate_psd(x, 512, 48000.0)
+        assert np.abs(d_p.cpu().numpy() - want).max() <= 1e-3
+        for bad in ((x, 500, 48000.0), (x[:100], 512, 48000.0), (x, 16384, 48000.0)):
+            with pytest.raises(fmrx.FmrxError):
+                rx.estimate_psd(*bad)
