@@ -69,18 +69,26 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # FMRX_BENCH_BACKEND=gloo rehearses the N>1 path where there are fewer GPUs than ranks
+    # (ranks share devices; barriers and the timing reduction go through gloo on the CPU).
+    # The data path has no collective either way: every rank owns an independent stream.
+    backend = os.environ.get("FMRX_BENCH_BACKEND", "nccl")
+    dev = local if backend == "nccl" else local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
 
     import iqgen
 
     fmrx = iqgen.load_fmrx()
-    rx = fmrx.Receiver(0, fmrx.MONO, rf_taps=RF_TAPS, device=local if world > 1 else 0)
+    rx = fmrx.Receiver(0, fmrx.MONO, rf_taps=RF_TAPS, device=dev if world > 1 else 0)
     bb, na = rx.geo.block_bytes, rx.geo.audio_frames
     nb = STREAM_BYTES // bb
     n_iq = nb * bb // 2
@@ -109,7 +117,7 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     kern_ms, launches = rx.kernel_timing(reset=-1)
     if dist is not None:
-        t = torch.tensor([elapsed, kern_ms], device="cuda", dtype=torch.float64)
+        t = torch.tensor([elapsed, kern_ms], device="cuda" if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 
@@ -165,7 +173,7 @@ def main() -> None:
         with open(traffic_file) as f:
             line["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
 
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the contract: rank 0 at N=1 only
         line["cpu_baseline"] = cpu_baseline(d_iq, d_pcm, args.cpu_sample_bytes, bb, na)
     if rank == 0:
         print(json.dumps(line), flush=True)
