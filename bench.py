@@ -34,18 +34,15 @@ STREAM_BYTES = 1 << 30         # BASELINE config 2: 1 GiB synthetic IQ
 RF_TAPS = 101
 
 
-# compiled variants of the fused kernel (csrc/mono_fused.hip kVariants), default index 9
+# compiled variants of the fused kernel (csrc/mono_fused.hip kVariants), default index 6
 _VARIANTS = ["mono_fused_kernel<101,10,5,256,3,3>", "mono_fused_kernel<101,10,5,128,3,3>",
              "mono_fused_kernel<101,10,5,64,3,3>", "mono_fused_kernel<101,10,5,128,5,3>",
-             "mono_fused_kernel<101,10,5,256,3,5>", "mono_wave_kernel<101,10,5,3,3>",
-             "mono_fused_kernel<101,10,5,64,3,3,PF=2>", "mono_fused_kernel<101,10,5,128,3,3,PF=2>",
-             "mono_fused_kernel<101,10,5,64,3,3,TR=1>", "mono_fused_kernel<101,10,5,64,3,4,TR=1>",
-             "mono_fused_kernel<101,10,5,64,3,4,TR=1,AK=2>", "mono_fused_kernel<101,10,5,64,3,4,AK=2>",
-             "mono_fused_kernel<101,10,5,64,2,4,DB1=1>", "mono_fused_kernel<101,10,5,64,2,3,DB1=1>"]
+             "mono_fused_kernel<101,10,5,256,3,5>", "mono_fused_kernel<101,10,5,64,3,3,TR=1>",
+             "mono_fused_kernel<101,10,5,64,3,4,TR=1>"]
 
 
 def kernel_name() -> str:
-    return _VARIANTS[int(os.environ.get("FMRX_MONO_VARIANT", "9"))]  # csrc kDefaultVariant
+    return _VARIANTS[int(os.environ.get("FMRX_MONO_VARIANT", "6"))]  # csrc kDefaultVariant
 
 
 def flops_per_iq(rf_taps: int) -> float:

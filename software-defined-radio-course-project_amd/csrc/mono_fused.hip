@@ -95,31 +95,24 @@ __device__ inline float sbyte(uint32_t w) {
 }
 
 // ABL (timing ablations only, never selected in production): bit 1 skips the RF FIR, 2 the
-// audio FIR, 4 the demod, 8 the byte conversion of the staging.
+// audio FIR, 4 the demod, 8 the byte conversion of the staging, 16 the global loads, 32 the
+// staging writes.
 // TR = 1 keeps the RF taps in VGPRs for the whole launch (the kernel is LDS-capped at two
 // waves per SIMD, which leaves the register file room for them) instead of re-reading them
-// from LDS once per chunk.
-// AK = 2 (single-wave workgroups only) runs the audio stage once per pair of chunks: each
-// lane then owns two outputs, m and m + NB, accumulated together in packed f32 ops, which
-// halves the audio stage's instructions; the neighbour I/Q for the demod comes by lane
-// shuffle instead of LDS, which pays for the larger demod window.
-// DB1 = 1 single-buffers the demod window (its 50-sample history is copied forward after
-// the audio stage) to save LDS for a third workgroup per SIMD.  Single-wave workgroups
-// (NT = 64) take the demod's neighbour I/Q by lane shuffle, multi-wave ones through LDS.
-template <int T, int D, int AD, int NT, int R, int PD, int ABL = 0, int PF = 1, int TR = 0, int AK = 1,
-          int DB1 = 0>
+// from LDS once per chunk.  Single-wave workgroups (NT = 64) take the demod's neighbour I/Q
+// by lane shuffle, larger ones through LDS.
+// Measured and dropped: prefetching two chunks ahead, the audio stage once per
+// two chunks in packed ops, a single-buffered demod window with R = 2 for three waves per
+// SIMD, the audio FIR pipelined into the RF tap loop, staggered workgroup starts.
+template <int T, int D, int AD, int NT, int R, int PD, int ABL = 0, int TR = 0>
 __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps taps) {
     using C = MonoCfg<T, D, AD, NT, R>;
     constexpr int CIF = C::CIF, P = C::P, H = C::H, S = C::S, G = C::G, NLD = C::NLD;
     constexpr int WH = C::WH, NG = C::NG;
-    static_assert(AK == 1 || (AK == 2 && NT == 64 && CIF >= kAH), "grouped audio: one wave, CIF >= 50");
-    constexpr int NB = ((2 * CIF + AD - 1) / AD + 1) / 2;  // AK = 2: output pairs per group
-    static_assert(AK == 1 || NB <= NT, "one output pair per lane");
-    static_assert(DB1 == 0 || (AK == 1 && NT == 64), "single demod buffer: one wave, per-chunk audio");
     constexpr bool kShfl = NT == 64;
 
     __shared__ float4 xb4[C::XB / 2 + 1];        // scaled (I,Q) pairs, two per float4
-    __shared__ float dbuf[DB1 ? 1 : 2][kAH + AK * CIF];  // demod window: 50 history + AK chunks
+    __shared__ float dbuf[2][kAH + CIF];         // demod window: 50 history + chunk
     __shared__ float2v pbuf[kShfl ? 1 : 2][kShfl ? 1 : NT + 1];  // last RF output per thread
     __shared__ float2 ctab2[NG + 1];             // (c[2j-1], c[2j]); c[-1] = 0
     __shared__ float atab[kAudioTaps + 1];       // audio taps
@@ -152,17 +145,16 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         const uint32_t w = load4(in, halo, ((long long)(c0 - 1) * P - H + 2 * i) * 2, total, hb) ^ 0x80808080u;
         xb4[C::slot(2 * i) / 2] = make_float4(sbyte<0>(w), sbyte<1>(w), sbyte<2>(w), sbyte<3>(w));
     }
-    // Input prefetch, PF chunks ahead: pf holds chunk c, pf2 (PF == 2) chunk c+1.
-    uint32_t pf[NLD], pf2[NLD];
-    // The prefetch is always the same coalesced dword loads, from a base clamped into the
-    // stream so that they never leave it; the few chunks that touch the halo or run past the
-    // end (c outside [0, c_full)) are rebuilt at staging time instead.  One load path keeps
-    // the loads asynchronous: with a second path the compiler merges the two sets of
-    // registers right after issue, behind an s_waitcnt that exposes the HBM latency.
-    auto fetch = [&](int cc, uint32_t (&dst)[NLD]) {
+    // Input prefetch, one chunk ahead.  It is always the same coalesced dword loads, from a
+    // base clamped into the stream so that they never leave it; the few chunks that touch
+    // the halo or run past the end (c outside [0, c_full)) are rebuilt at staging time.  One
+    // load path keeps the loads asynchronous: with a second path the compiler merges the two
+    // register sets right after issue, behind an s_waitcnt that exposes the HBM latency.
+    uint32_t pf[NLD];
+    auto fetch = [&](int cc) {
         if constexpr ((ABL & 16) != 0) {  // ablation: no global loads
 #pragma unroll
-            for (int l = 0; l < NLD; l++) dst[l] = (uint32_t)(cc * 77 + l * 77 + tid);
+            for (int l = 0; l < NLD; l++) pf[l] = (uint32_t)(cc * 77 + l * 77 + tid);
             return;
         }
         if (c_full == 0) return;  // stream shorter than a chunk: every chunk is rebuilt
@@ -170,12 +162,9 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         const uint32_t* src = reinterpret_cast<const uint32_t*>(in + (size_t)cl * (2 * P)) + tid;
 #pragma unroll
         for (int l = 0; l < NLD; l++)
-            if ((P / 2) % NT == 0 || tid + l * NT < P / 2) dst[l] = src[l * NT];
+            if ((P / 2) % NT == 0 || tid + l * NT < P / 2) pf[l] = src[l * NT];
     };
-    fetch(c0 - 1, pf);
-    if constexpr (PF == 2) {
-        if (c0 < c1) fetch(c0, pf2);
-    }
+    fetch(c0 - 1);
 
     float2 creg[TR ? NG : 1];
     if constexpr (TR != 0) {
@@ -188,20 +177,23 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     // increment turns into (0, 0), and ar is only read for c >= c0.
     long long aq = (long long)(c0 - 1) * CIF / AD;
     int ar = (int)((long long)(c0 - 1) * CIF - aq * AD);
-    long long gaq = 0;  // AK = 2: (aq, ar) of the current group's first audio chunk
-    int gar = 0;
-    float2v carry = {0.0f, 0.0f};  // AK = 2: last RF output of the previous chunk
+    float2v carry = {0.0f, 0.0f};  // NT = 64: last RF output of the previous chunk
     for (int c = c0 - 1; c < c1; c++) {
         // ---- stage chunk c: lane u writes pairs H+2u, H+2u+1 as one float4; consecutive
         // lanes write consecutive 16-B slots (conflict-free ds_write_b128).
-        const bool edge = (ABL & 16) == 0 && !(c >= 0 && c < c_full);
+        if ((ABL & 16) == 0 && !(c >= 0 && c < c_full)) {
+            // rare (one uniform branch): rebuild this chunk's words from the halo / padding
+#pragma unroll
+            for (int l = 0; l < NLD; l++) {
+                const int u = tid + l * NT;
+                if ((P / 2) % NT == 0 || u < P / 2) pf[l] = load4(in, halo, (long long)c * (2 * P) + 4LL * u, total, hb);
+            }
+        }
 #pragma unroll
         for (int l = 0; l < NLD; l++) {
             const int u = tid + l * NT;
             if ((P / 2) % NT == 0 || u < P / 2) {
-                uint32_t raw = pf[l];
-                if (edge) raw = load4(in, halo, (long long)c * (2 * P) + 4LL * u, total, hb);
-                const uint32_t w = raw ^ 0x80808080u;
+                const uint32_t w = pf[l] ^ 0x80808080u;
                 if constexpr ((ABL & 32) != 0) {  // ablation: no staging writes
                     asm volatile("" ::"v"(w));
                     continue;
@@ -213,21 +205,14 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
             }
         }
         __syncthreads();  // (A) chunk c staged, carry from c-1 in place
-        if constexpr (PF == 2) {
-#pragma unroll
-            for (int l = 0; l < NLD; l++) pf[l] = pf2[l];
-            if (c + 2 < c1) fetch(c + 2, pf2);
-        } else {
-            if (c + 1 < c1) fetch(c + 1, pf);
-        }
+        if (c + 1 < c1) fetch(c + 1);
 
         // ---- RF LPF + decimate.  Thread t owns outputs j = R t + r, r < R, whose samples are
         // window offsets o = D r + T-1-k (window base pair S t).  Tap-outer order: at tap k all
         // R outputs take their k-th term, so each output is still an ascending-k sequential
         // sum, while samples slide through a register window (each LDS pair read once per
-        // thread) and taps come as broadcast LDS pairs.  Group 0 = tap 0, group j = taps
-        // 2j-1, 2j; group j's new samples are the pair (T-1-2j, T-2j); loads run PD groups
-        // ahead of use.
+        // thread).  Group 0 = tap 0, group j = taps 2j-1, 2j; group j's new samples are the
+        // pair (T-1-2j, T-2j); loads run PD groups ahead of use.
         if constexpr (TR != 0) {
             // Opaque per chunk, so LICM cannot hoist 101 loop-invariant (c, c) splats out of
             // the chunk loop; the products then broadcast a tap with op_sel instead.
@@ -294,10 +279,10 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         // ---- carries for chunk c+1: RF history (pairs [P, P+H) -> [0, H)) as aligned 16-B
         // pair groups (P and H are even, so groups never straddle a pad), last I/Q
         for (int i = tid; i < H / 2; i += NT) xb4[C::slot(2 * i) / 2] = xb4[C::slot(P + 2 * i) / 2];
-        float2v prev;
+        float2v prev;  // FM demod's previous I/Q: the neighbouring thread's / previous chunk's
         if constexpr (!kShfl) {
             if (tid == 0) pbuf[cur ^ 1][0] = pbuf[cur][NT];
-            prev = pbuf[cur][tid];  // FM demod's previous I/Q: neighbouring thread / chunk
+            prev = pbuf[cur][tid];
         } else {
             prev.x = __shfl_up(acc[R - 1].x, 1);
             prev.y = __shfl_up(acc[R - 1].y, 1);
@@ -315,14 +300,11 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                 d[r] = fm_demod_one(acc[r].x, acc[r].y, pv.x, pv.y);
         }
         const long long g0 = (long long)c * CIF + R * tid;  // IF index of d[0]
-        // AK = 2: chunk c is slot q of its group (groups start at the pre-roll chunk); the
-        // group's last 50 samples also go to the other buffer as the next group's history.
-        const int q = AK == 1 ? 0 : (int)((c - (c0 - 1)) & 1);
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const int jl = R * tid + r;
-            dbuf[DB1 ? 0 : cur][kAH + q * CIF + jl] = d[r];
-            if (!DB1 && (AK == 1 || q == 1) && jl >= CIF - kAH) dbuf[DB1 ? 0 : cur ^ 1][jl - (CIF - kAH)] = d[r];
+            dbuf[cur][kAH + jl] = d[r];
+            if (jl >= CIF - kAH) dbuf[cur ^ 1][jl - (CIF - kAH)] = d[r];
         }
         // Demod to global only for the split API / the chunk holding the stream's last 50
         // samples (one scalar test per chunk; the fused mono path skips it otherwise).
@@ -340,49 +322,16 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         }
         __syncthreads();  // (C) demod window complete
 
-        // ---- audio LPF + decimate + quantise: outputs m with AD*m in this chunk
-        // Chunk c starts at IF index pos = c CIF = AD aq + ar (tracked incrementally); its
-        // first audio output is m0 = aq + (ar > 0), at chunk offset off0 = AD m0 - pos.
-        if constexpr (AK == 2) {
-            // group audio start: chunk gs = max(cs, c0), where cs = c - q starts the group
-            if (c >= c0 && (q == 0 || c == c0)) { gaq = aq; gar = ar; }
-            if (L.audio && c >= c0 && (q == 1 || c == c1 - 1)) {
-                const int gsrel = (c - q < c0) ? 1 : 0;          // gs - cs
-                const int off0 = gar > 0 ? AD - gar : 0;
-                const long long m0 = gaq + (gar > 0);
-                const int span = (q + 1 - gsrel) * CIF;          // IF samples with audio
-                const long long left = n_audio - m0;
-                const int cnt = (int)std::min<long long>((span - off0 + AD - 1) / AD, left);
-                if (tid < NB && cnt > 0) {
-                    // clamp idle lanes onto valid samples; their sums are not stored
-                    const int ia = kAH + gsrel * CIF + off0 + AD * min(tid, cnt - 1);
-                    const float* dw = &dbuf[cur][ia];
-                    const int db = AD * (min(NB + tid, cnt - 1) - min(tid, cnt - 1));
-                    float2v a2 = {0.0f, 0.0f};
-#pragma unroll
-                    for (int k = 0; k < ((ABL & 2) != 0 ? 1 : kAudioTaps); k++) {
-                        const float2v p = float2v{dw[-k], dw[db - k]} * atab[k];
-                        a2 = a2 + p;
-                    }
-                    const size_t oi = (size_t)stream * (size_t)n_audio + (size_t)m0 + tid;
-                    if (tid < cnt) {
-                        L.pcm[oi] = quantize_s16(a2.x);
-                        if (L.mono) L.mono[oi] = a2.x;
-                    }
-                    if (NB + tid < cnt) {
-                        L.pcm[oi + NB] = quantize_s16(a2.y);
-                        if (L.mono) L.mono[oi + NB] = a2.y;
-                    }
-                }
-            }
-            if (q == 1) cur ^= 1;
-        } else if (L.audio && c >= c0) {
+        // ---- audio LPF + decimate + quantise: outputs m with AD*m in this chunk.  Chunk c
+        // starts at IF index pos = c CIF = AD aq + ar (tracked incrementally); its first audio
+        // output is m0 = aq + (ar > 0), at chunk offset off0 = AD m0 - pos.
+        if (L.audio && c >= c0) {
             const int off0 = ar > 0 ? AD - ar : 0;
             const long long m0 = aq + (ar > 0);
             const long long left = n_audio - m0;  // outputs of the stream not yet written
             if (tid < C::CAmax && off0 + AD * tid < CIF && tid < left) {
                 const long long m = m0 + tid;
-                const float* dw = &dbuf[DB1 ? 0 : cur][off0 + AD * tid + kAH];
+                const float* dw = &dbuf[cur][off0 + AD * tid + kAH];
                 float a = 0.0f;
 #pragma unroll
                 for (int k = 0; k < ((ABL & 2) != 0 ? 1 : kAudioTaps); k++) {
@@ -394,264 +343,28 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                 if (L.mono) L.mono[oi] = a;
             }
         }
-        if constexpr (DB1 != 0) {
-            // history for chunk c+1; one wave: its LDS operations complete in issue order,
-            // so these writes land after the audio reads above
-            if (tid < kAH) {
-                const float h = dbuf[0][CIF + tid];
-                dbuf[0][tid] = h;
-            }
-        }
-        if constexpr (AK == 1) cur ^= 1;
+        cur ^= 1;
         aq += CIF / AD;
         ar += CIF % AD;
         if (ar >= AD) { ar -= AD; aq++; }
     }
 }
 
-// ---- single-wave variant with a software-pipelined audio stage -------------------------
-// A 64-thread workgroup is one wave, so its "barriers" are free and lanes can trade values
-// through cross-lane shuffles.  The audio FIR of chunk c-1 (a 51-step dependent chain that
-// would otherwise run alone after the RF stage) is interleaved into chunk c's RF tap loop,
-// APG taps per tap group, where the RF's independent work hides its latency.
-template <int T, int D, int AD, int R, int PD>
-__global__ void __launch_bounds__(64) mono_wave_kernel(MonoLaunch L, MonoTaps taps) {
-    constexpr int NT = 64;
-    using C = MonoCfg<T, D, AD, NT, R>;
-    constexpr int CIF = C::CIF, P = C::P, H = C::H, S = C::S, G = C::G, NLD = C::NLD;
-    constexpr int WH = C::WH, NG = C::NG;
-    constexpr int APG = (kAudioTaps + NG - 1) / NG;  // audio taps per RF tap group
-    constexpr int TR = 0;                             // taps re-read from LDS (see fused kernel)
-    float2 creg[1] = {};
-    static_assert(C::CAmax <= NT, "one audio output per lane per chunk");
-
-    __shared__ float4 xb4[C::XB / 2 + 1];
-    __shared__ float dbuf[2][kAH + CIF];
-    __shared__ float2 ctab2[NG + 1];
-    __shared__ float atab[APG * NG + 1];
-    float2v* xb = reinterpret_cast<float2v*>(xb4);
-    float* ctab = reinterpret_cast<float*>(ctab2);
-
-    const int tid = threadIdx.x;
-    const int stream = blockIdx.x / L.segs;
-    const int seg = blockIdx.x - stream * L.segs;
-    const long long n_if = L.n_if;
-    const long long n_chunks = (n_if + CIF - 1) / CIF;
-    const long long c0 = seg * n_chunks / L.segs;
-    const long long c1 = (seg + 1) * n_chunks / L.segs;
-    if (c0 >= c1) return;
-    const long long n_audio = n_if / AD;
-
-    const uint8_t* in = L.iq + (size_t)stream * L.stream_bytes;
-    const uint8_t* halo = L.halo + (size_t)stream * L.halo_bytes;
-    const long long total = (long long)L.stream_bytes;
-    const long long hb = (long long)L.halo_bytes;
-
-    for (int i = tid; i < 2 * (NG + 1); i += NT) ctab[i] = (i >= 1 && i <= T) ? taps.rf[i - 1] : 0.0f;
-    for (int i = tid; i < APG * NG + 1; i += NT) atab[i] = i < kAudioTaps ? taps.audio[i] : 0.0f;
-    for (int i = tid; i < H / 2; i += NT) {
-        const uint32_t w = load4(in, halo, ((c0 - 1) * (long long)P - H + 2 * i) * 2, total, hb) ^ 0x80808080u;
-        xb4[C::slot(2 * i) / 2] = make_float4(sbyte<0>(w), sbyte<1>(w), sbyte<2>(w), sbyte<3>(w));
-    }
-    uint32_t pf[NLD];
-#pragma unroll
-    for (int l = 0; l < NLD; l++) {
-        const int u = tid + l * NT;
-        if (u < P / 2) pf[l] = load4(in, halo, (c0 - 1) * 2LL * P + 4LL * u, total, hb);
-    }
-
-    // audio output owned by this lane for chunk a: m = ceil(a CIF / AD) + tid
-    auto audio_slot = [&](long long a, bool& active) -> long long {
-        const long long m = (a * CIF + AD - 1) / AD + tid;
-        active = L.audio && a >= c0 && tid < C::CAmax && AD * m < (a + 1) * CIF && m < n_audio;
-        return m;
-    };
-    auto audio_store = [&](long long m, float acc) {
-        const size_t oi = (size_t)stream * (size_t)n_audio + (size_t)m;
-        L.pcm[oi] = quantize_s16(acc);
-        if (L.mono) L.mono[oi] = acc;
-    };
-
-    float2v carry = {0.0f, 0.0f};  // last RF output of the previous chunk (uniform)
-    int cur = 0;
-    for (long long c = c0 - 1; c < c1; c++) {
-#pragma unroll
-        for (int l = 0; l < NLD; l++) {
-            const int u = tid + l * NT;
-            if ((P / 2) % NT == 0 || u < P / 2) {
-                const uint32_t w = pf[l] ^ 0x80808080u;
-                xb4[C::slot(H + 2 * u) / 2] = make_float4(sbyte<0>(w), sbyte<1>(w), sbyte<2>(w), sbyte<3>(w));
-            }
-        }
-        __syncthreads();  // staging (and the previous chunk's demod window) visible
-        if (c + 1 < c1) {
-            const long long nb0 = (c + 1) * 2LL * P;
-            if (nb0 + 2LL * P <= total) {
-                const uint32_t* src = reinterpret_cast<const uint32_t*>(in + nb0) + tid;
-#pragma unroll
-                for (int l = 0; l < NLD; l++)
-                    if ((P / 2) % NT == 0 || tid + l * NT < P / 2) pf[l] = src[l * NT];
-            } else {
-#pragma unroll
-                for (int l = 0; l < NLD; l++) {
-                    const int u = tid + l * NT;
-                    if (u < P / 2) pf[l] = load4(in, halo, nb0 + 4LL * u, total, hb);
-                }
-            }
-        }
-
-        // audio of chunk c-1 (window in dbuf[cur^1]), run inside the RF loop below
-        bool a_on;
-        const long long am = audio_slot(c - 1, a_on);
-        const int aoff = a_on ? (int)(AD * am - (c - 1) * CIF + kAH) : kAH;
-        const float* dw = &dbuf[cur ^ 1][aoff];
-        float aacc = 0.0f;
-
-        float2v acc[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) acc[r] = float2v{0.0f, 0.0f};
-        int zero;
-        asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
-        const float2* cb = ctab2 + zero;
-        const float* ab = atab + zero;
-        float2v X[WH + 3];
-        float2 cc[NG];
-        float av[NG * APG], aw[NG * APG];
-        const float4* wb = xb4 + ((S + G) / 2) * tid;
-        auto ld = [&](int o) {
-            const float4 q = wb[(o + G * (o / S)) / 2];
-            X[o] = float2v{q.x, q.y};
-            X[o + 1] = float2v{q.z, q.w};
-        };
-        auto ldg = [&](int j) {
-            if (j < NG) {
-                if constexpr (TR == 0) cc[j] = cb[j];
-                if (j >= 1) ld(T - 1 - 2 * j);
-#pragma unroll
-                for (int h = 0; h < APG; h++) {
-                    const int k = j * APG + h;
-                    if (k < kAudioTaps) {
-                        aw[k] = ab[k];
-                        av[k] = dw[-k];
-                    }
-                }
-            }
-        };
-#pragma unroll
-        for (int o = T - 1; o <= WH; o += 2) ld(o);
-#pragma unroll
-        for (int j = 0; j < PD; j++) ldg(j);
-#pragma unroll
-        for (int j = 0; j < NG; j++) {
-            ldg(j + PD);
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int k = 2 * j - 1 + h;
-                if (k >= 0) {
-                    const float2 cj = TR ? creg[TR ? j : 0] : cc[j];
-                    const float ck = h == 0 ? cj.x : cj.y;
-#pragma unroll
-                    for (int r = 0; r < R; r++) {
-                        const float2v p = X[T - 1 - k + D * r] * ck;
-                        acc[r] = acc[r] + p;
-                    }
-                }
-            }
-#pragma unroll
-            for (int h = 0; h < APG; h++) {
-                const int k = j * APG + h;
-                if (k < kAudioTaps) {
-                    const float p = aw[k] * av[k];
-                    aacc = aacc + p;
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            asm volatile("" ::"v"(acc[r]));
-            acc[r] = acc[r] * 0.0078125f;
-        }
-        asm volatile("" ::"v"(aacc));
-        if (a_on) audio_store(am, aacc);
-
-        // carries for chunk c+1 (same wave: the RF reads above are complete in order)
-        for (int i = tid; i < H; i += NT) xb[C::slot(i)] = xb[C::slot(P + i)];
-
-        // FM demod: previous output from the neighbouring lane / previous chunk
-        float2v prev;
-        prev.x = __shfl_up(acc[R - 1].x, 1);
-        prev.y = __shfl_up(acc[R - 1].y, 1);
-        if (tid == 0) prev = carry;
-        carry.x = __shfl(acc[R - 1].x, NT - 1);
-        carry.y = __shfl(acc[R - 1].y, NT - 1);
-        float d[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            const float2v pv = r == 0 ? prev : acc[r - 1];
-            d[r] = fm_demod_one(acc[r].x, acc[r].y, pv.x, pv.y);
-        }
-        const long long g0 = c * CIF + R * tid;
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            const int jl = R * tid + r;
-            dbuf[cur][kAH + jl] = d[r];
-            if (jl >= CIF - kAH) dbuf[cur ^ 1][jl - (CIF - kAH)] = d[r];
-        }
-        if (c >= c0 && (L.demod || L.demod_tail)) {
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const long long g = g0 + r;
-                if (g < n_if) {
-                    if (L.demod)
-                        L.demod[(size_t)stream * L.demod_stride + L.demod_hist + g] = d[r];
-                    if (L.demod_tail && g >= n_if - kAH)
-                        L.demod_tail[(size_t)stream * kAH + (g - (n_if - kAH))] = d[r];
-                }
-            }
-        }
-        cur ^= 1;
-    }
-    // epilogue: audio of the last chunk (window in dbuf[cur^1] after the final toggle)
-    __syncthreads();
-    bool a_on;
-    const long long am = audio_slot(c1 - 1, a_on);
-    if (a_on) {
-        const float* dw = &dbuf[cur ^ 1][AD * am - (c1 - 1) * CIF + kAH];
-        float a = 0.0f;
-        for (int k = 0; k < kAudioTaps; k++) {
-            const float p = atab[k] * dw[-k];
-            a = a + p;
-        }
-        audio_store(am, a);
-    }
-}
-
-template <int T, int D, int AD, int R, int PD>
-int launch_wave(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStream_t s) {
-    hipLaunchKernelGGL((mono_wave_kernel<T, D, AD, R, PD>), dim3(n_streams * L.segs), dim3(64), 0, s, L, taps);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-
-template <int T, int D, int AD, int NT, int R, int PD, int PF = 1, int TR = 0, int AK = 1, int DB1 = 0>
+template <int T, int D, int AD, int NT, int R, int PD, int TR = 0>
 int launch_variant(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStream_t s) {
-    const dim3 grid(n_streams * L.segs), block(NT);
-    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD, 0, PF, TR, AK, DB1>), grid, block, 0, s, L, taps);
+    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD, 0, TR>), dim3(n_streams * L.segs), dim3(NT), 0,
+                       s, L, taps);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-// Tunables.  The default was picked by measurement on MI355X (tools/tune_mono.py); other
+// Tunables.  The default was picked by measurement on MI355X (tools/tune_list.py); the other
 // variants stay compiled for the tuning sweep (FMRX_MONO_VARIANT=<index>).
 struct Variant {
-    int nt, r, pd, wg_per_cu;  // wg_per_cu: resident workgroups per CU (LDS-limited)
+    int nt, r, pd, tr, wg_per_cu;  // wg_per_cu: resident workgroups per CU (LDS-limited)
 };
-constexpr Variant kVariants[] = {{256, 3, 3, 2}, {128, 3, 3, 4}, {64, 3, 3, 8}, {128, 5, 3, 3},
-                                 {256, 3, 5, 2}, {64, 3, 3, 8}, {64, 3, 3, 8}, {128, 3, 3, 4},
-                                 {64, 3, 3, 8}, {64, 3, 4, 8},  // 8, 9: taps in VGPRs
-                                 {64, 3, 4, 8}, {64, 3, 4, 8},  // 10: + paired audio; 11: paired audio
-                                 {64, 2, 4, 12}, {64, 2, 3, 12}};  // 12, 13: R=2, 3 waves/SIMD
-// 5: mono_wave_kernel; 6, 7: input prefetched two chunks ahead
-constexpr int kDefaultVariant = 9;  // 64-thread workgroups (waves never wait on each other), taps in VGPRs
+constexpr Variant kVariants[] = {{256, 3, 3, 0, 2}, {128, 3, 3, 0, 4}, {64, 3, 3, 0, 8}, {128, 5, 3, 0, 3},
+                                 {256, 3, 5, 0, 2}, {64, 3, 3, 1, 8}, {64, 3, 4, 1, 8}};
+constexpr int kDefaultVariant = 6;  // one wave per workgroup, taps in VGPRs, 4 groups of prefetch
 
 int variant_index() {  // FMRX_MONO_VARIANT: tuning sweeps only
     static int v = [] {
@@ -689,8 +402,8 @@ int ablation() {
 
 template <int ABL>
 int launch_ablation(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStream_t s) {
-    hipLaunchKernelGGL((mono_fused_kernel<101, 10, 5, 64, 3, 4, ABL, 1, 1>), dim3(n_streams * L.segs),
-                       dim3(64), 0, s, L, taps);
+    hipLaunchKernelGGL((mono_fused_kernel<101, 10, 5, 64, 3, 4, ABL, 1>), dim3(n_streams * L.segs), dim3(64), 0,
+                       s, L, taps);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -703,45 +416,26 @@ int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_de
             case 2: return launch_ablation<2>(L, n_streams, taps, s);
             case 4: return launch_ablation<4>(L, n_streams, taps, s);
             case 8: return launch_ablation<8>(L, n_streams, taps, s);
-            case 6: return launch_ablation<6>(L, n_streams, taps, s);
-            case 14: return launch_ablation<14>(L, n_streams, taps, s);
             case 15: return launch_ablation<15>(L, n_streams, taps, s);
             case 16: return launch_ablation<16>(L, n_streams, taps, s);
-            case 31: return launch_ablation<31>(L, n_streams, taps, s);
-            case 47: return launch_ablation<47>(L, n_streams, taps, s);
-            case 63: return launch_ablation<63>(L, n_streams, taps, s);
-            case 62: return launch_ablation<62>(L, n_streams, taps, s);
             case 30: return launch_ablation<30>(L, n_streams, taps, s);
+            case 31: return launch_ablation<31>(L, n_streams, taps, s);
+            case 62: return launch_ablation<62>(L, n_streams, taps, s);
+            case 63: return launch_ablation<63>(L, n_streams, taps, s);
             default: break;
         }
     }
-#define FMRX_V(T_, D_, AD_, I_, NT_, R_, PD_)                                              \
+#define FMRX_V(T_, D_, AD_, I_, NT_, R_, PD_, TR_)                                         \
     if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == I_)                  \
-        return launch_variant<T_, D_, AD_, NT_, R_, PD_>(L, n_streams, taps, s);
-#define FMRX_ALL(T_, D_, AD_)           \
-    FMRX_V(T_, D_, AD_, 0, 256, 3, 3)   \
-    FMRX_V(T_, D_, AD_, 1, 128, 3, 3)   \
-    FMRX_V(T_, D_, AD_, 2, 64, 3, 3)    \
-    FMRX_V(T_, D_, AD_, 3, 128, 5, 3)   \
-    FMRX_V(T_, D_, AD_, 4, 256, 3, 5)   \
-    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 5) \
-        return launch_wave<T_, D_, AD_, 3, 3>(L, n_streams, taps, s);    \
-    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 6) \
-        return launch_variant<T_, D_, AD_, 64, 3, 3, 2>(L, n_streams, taps, s); \
-    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 7) \
-        return launch_variant<T_, D_, AD_, 128, 3, 3, 2>(L, n_streams, taps, s); \
-    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 8) \
-        return launch_variant<T_, D_, AD_, 64, 3, 3, 1, 1>(L, n_streams, taps, s); \
-    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 9) \
-        return launch_variant<T_, D_, AD_, 64, 3, 4, 1, 1>(L, n_streams, taps, s); \
-    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 10) \
-        return launch_variant<T_, D_, AD_, 64, 3, 4, 1, 1, 2>(L, n_streams, taps, s); \
-    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 11) \
-        return launch_variant<T_, D_, AD_, 64, 3, 4, 1, 0, 2>(L, n_streams, taps, s); \
-    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 12) \
-        return launch_variant<T_, D_, AD_, 64, 2, 4, 1, 0, 1, 1>(L, n_streams, taps, s); \
-    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == 13) \
-        return launch_variant<T_, D_, AD_, 64, 2, 3, 1, 0, 1, 1>(L, n_streams, taps, s);
+        return launch_variant<T_, D_, AD_, NT_, R_, PD_, TR_>(L, n_streams, taps, s);
+#define FMRX_ALL(T_, D_, AD_)              \
+    FMRX_V(T_, D_, AD_, 0, 256, 3, 3, 0)   \
+    FMRX_V(T_, D_, AD_, 1, 128, 3, 3, 0)   \
+    FMRX_V(T_, D_, AD_, 2, 64, 3, 3, 0)    \
+    FMRX_V(T_, D_, AD_, 3, 128, 5, 3, 0)   \
+    FMRX_V(T_, D_, AD_, 4, 256, 3, 5, 0)   \
+    FMRX_V(T_, D_, AD_, 5, 64, 3, 3, 1)    \
+    FMRX_V(T_, D_, AD_, 6, 64, 3, 4, 1)
     FMRX_ALL(51, 10, 5)    // mode 0 (and mode 2's RF stage), reference taps
     FMRX_ALL(101, 10, 5)   // mode 0, 101-tap RF (BASELINE configs[1])
     FMRX_ALL(51, 4, 6)     // mode 1
