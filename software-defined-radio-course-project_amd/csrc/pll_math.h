@@ -43,6 +43,16 @@ FMRX_HD bool decide_float(double r, double e, float* out) {
     return lo == hi;
 }
 
+// Integer form of the same test for a value known to |v| (1 + 13.5 ulp): the float rounding
+// drops the low 29 bits of the double; it is unambiguous unless those bits lie within 16 ulps
+// of the halfway point 2^28.  (A bound crossing a float exactly or a binade edge still rounds
+// to the same float, so only the halfway point matters.)  3 integer ops instead of ~8.
+FMRX_HD bool decide_float_16ulp(double v, float* out) {
+    *out = (float)v;
+    const uint32_t t = (uint32_t)__builtin_bit_cast(uint64_t, v) & 0x1FFFFFFFu;
+    return t - (0x10000000u - 16u) > 32u;
+}
+
 // sin and cos of a float argument, results rounded to float.  Returns false when the fast
 // path cannot certify the rounding (caller falls back).
 FMRX_HD bool fast_sincos_f(float xf, float* s_out, float* c_out) {
@@ -185,13 +195,17 @@ FMRX_HD bool sincos_ctx_f(float xf, float* s_out, float* c_out, PllCtx* ctx) {
     const double sn = fma(z * r, ps, r);
     const double pc = fma(z4, fma(z, kC6, kC5), fma(z2, fma(z, kC4, kC3), fma(z, kC2, kC1)));
     const double cs = 1.0 - (0.5 * z - (z * z) * pc);
-    const int q = (int)((long long)nd & 3);
+    const int q = (int)nd & 3;  // |nd| < 6.4e8 fits an int; & 3 is mod 4 for negatives too
     const double sv = (q & 1) ? cs : sn, cv0 = (q & 1) ? sn : cs;
-    const double s2 = (q & 2) ? -sv : sv;
-    const double c2 = ((q + 1) & 2) ? -cv0 : cv0;
-    const double ea = fabs(nd) * 1.0e-32;
-    const bool s_ok = decide_float(s2, 1.5e-15 * fabs(s2) + ea, s_out);
-    const bool c_ok = decide_float(c2, 1.5e-15 * fabs(c2) + ea, c_out);
+    // quadrant signs as sign-bit flips (q & 2 for sin, (q + 1) & 2 for cos)
+    const double s2 = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, sv) ^ ((uint64_t)(q & 2) << 62));
+    const double c2 =
+        __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, cv0) ^ ((uint64_t)((q + 1) & 2) << 62));
+    // Certified rounding: relative error <= 1.5e-15 (13.5 ulp), and the absolute reduction
+    // term |nd| 1e-32 stays below 0.03 ulp for |v| >= 2^-20 -> a 16-ulp window; smaller
+    // results (probability ~1e-6 per call) take the library path.
+    const bool s_ok = (int)decide_float_16ulp(s2, s_out) & (int)(fabs(s2) >= 0x1p-20);
+    const bool c_ok = (int)decide_float_16ulp(c2, c_out) & (int)(fabs(c2) >= 0x1p-20);
     // (C, S, r, q) are within the bounds rot_atan2_f assumes whether or not the float
     // rounding could be certified here, so the context is valid either way.
     ctx->C = c2;

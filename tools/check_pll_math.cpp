@@ -19,7 +19,7 @@
 static float bits2f(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 static uint32_t f2bits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
 
-struct Count { unsigned long long n = 0, fast = 0, fb = 0, bad = 0; };
+struct Count { unsigned long long n = 0, fast = 0, fb = 0, fb2 = 0, bad = 0; };
 
 static uint64_t sm64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -54,6 +54,18 @@ int main(int argc, char** argv) {
                             }
                         } else {
                             c.fb++;
+                        }
+                        // the PLL's own path (context-producing sincos, integer certification)
+                        fmrx::PllCtx ctx{};
+                        float s2, c2;
+                        if (fmrx::sincos_ctx_f(x, &s2, &c2, &ctx)) {
+                            const float gs = (float)std::sin((double)x), gc = (float)std::cos((double)x);
+                            if (f2bits(s2) != f2bits(gs) || f2bits(c2) != f2bits(gc)) {
+                                if (c.bad < 5) std::printf("MISMATCH sincos_ctx x=%.9g fast=(%.9g,%.9g) glibc=(%.9g,%.9g)\n", x, s2, c2, gs, gc);
+                                c.bad++;
+                            }
+                        } else {
+                            c.fb2++;
                         }
                     }
                 }
@@ -94,7 +106,8 @@ int main(int argc, char** argv) {
     }
     for (auto& t : th) t.join();
     Count s;
-    for (auto& c : cnt) { s.n += c.n; s.fast += c.fast; s.fb += c.fb; s.bad += c.bad; }
-    std::printf("%s checked=%llu fast=%llu fallback=%llu mismatches=%llu\n", argv[1], s.n, s.fast, s.fb, s.bad);
+    for (auto& c : cnt) { s.n += c.n; s.fast += c.fast; s.fb += c.fb; s.fb2 += c.fb2; s.bad += c.bad; }
+    std::printf("%s checked=%llu fast=%llu fallback=%llu ctx_fallback=%llu mismatches=%llu\n", argv[1], s.n, s.fast,
+                s.fb, s.fb2, s.bad);
     return s.bad ? 1 : 0;
 }
