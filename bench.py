@@ -172,6 +172,7 @@ def main() -> None:
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the contract: rank 0 at N=1 only
         line["cpu_baseline"] = cpu_baseline(d_iq, d_pcm, args.cpu_sample_bytes, bb, na)
+        line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(d_iq, args.cpu_sample_bytes, bb)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
@@ -212,6 +213,45 @@ def cpu_baseline(d_iq, d_pcm, sample_bytes, bb, na):
             "sample": f"first {nbs} blocks ({nbs * bb} B, {nbs * bb / 2 / RT_RATE:.1f} s of signal) "
                       f"of the rank-0 stream, sequential mono path",
             "seconds": round(dt, 2), "bit_exact_vs_gpu": parity}
+
+
+def _ref_worker(args):
+    """One host core: the reference mono path over one contiguous slice (its own stream)."""
+    chunk, barrier = args
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    ref = oracle.Reference()
+    barrier.wait()
+    t0 = time.perf_counter()
+    ref.run_mono(0, RF_TAPS, chunk)
+    return t0, time.perf_counter()
+
+
+def cpu_baseline_all_cores(d_iq, sample_bytes, bb):
+    """the reference's mono path with one stream per host core, all at once.
+    The GiB is cut into one contiguous slice per core (each slice an independent stream, so
+    only the timing is meaningful); spawned processes, no GPU.  Rate = bytes / wall span."""
+    import multiprocessing as mp
+
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    if not oracle.reference_available():
+        return None
+    cores = max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
+    nbs = sample_bytes // bb
+    host = d_iq[: nbs * bb].cpu().numpy()
+    per = nbs // cores
+    ctx = mp.get_context("spawn")
+    with ctx.Manager() as mgr:
+        barrier = mgr.Barrier(cores)
+        with ctx.Pool(cores) as pool:
+            spans = pool.map(_ref_worker, [(host[i * per * bb:(i + 1) * per * bb], barrier) for i in range(cores)])
+    dt = max(t1 for _, t1 in spans) - min(t0 for t0, _ in spans)
+    return {"value": round(cores * per * bb / 2 / dt / 1e6, 2), "unit": "MS/s", "cores": cores, "kind": "reference",
+            "sample": f"{cores} contiguous slices of {per} blocks, one process per core, concurrently",
+            "seconds": round(dt, 3)}
 
 
 if __name__ == "__main__":

@@ -1,0 +1,46 @@
+"""bench.py's output contract (the driver parses this line every round): one JSON line with
+the metric, whole-job value, timing fields, roofline and the CPU baseline keys.  A short run
+(2 steps, 1 warmup) on the GPU, in a child process (it owns the device while it runs)."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _run(*extra):
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1", *extra],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_json_contract():
+    j = _run("--no-cpu-baseline")
+    for k, t in (("metric", str), ("value", float), ("unit", str), ("n_gpus", int), ("steps", int),
+                 ("warmup", int), ("ms_per_step", float), ("higher_is_better", bool), ("scaling", str),
+                 ("dtype", str), ("data", str), ("config", dict), ("roofline", dict)):
+        assert isinstance(j[k], t), k
+    assert j["n_gpus"] == 1 and j["steps"] == 2 and j["warmup"] == 1 and j["scaling"] == "weak"
+    assert j["vs_baseline"] is None and j["higher_is_better"] is True
+    assert "workload" in j["config"]
+    rf = j["roofline"]
+    assert rf["bound"] in ("hbm", "mfma") and rf["unit"] in ("GB/s", "TFLOP/s")
+    assert 0 < rf["frac"] < 1 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    # value = IQ pairs of the whole job / wall time; the kernel alone is faster than a step
+    assert j["value"] > 1e5 and rf["kernel_ms"] <= j["ms_per_step"] * 1.05
+
+
+def test_bench_cpu_baseline_keys():
+    j = _run("--cpu-sample-bytes", str(64 * 12800))
+    cb = j["cpu_baseline"]
+    assert cb["kind"] in ("reference", "port") and cb["cores"] == 1 and cb["value"] > 0
+    assert cb["bit_exact_vs_gpu"] is True
