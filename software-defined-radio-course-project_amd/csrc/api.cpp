@@ -117,6 +117,8 @@ struct fmrx_ctx {
 
 namespace {
 
+constexpr int kAudioHist50 = 50;  // demod samples a resampler output reads before its base
+
 // Serialises the entry points of one context (rf and audio stages may be driven from two
 // threads, as project.cpp does; they share the context's stream and scratch buffers).
 class CtxLock {
@@ -244,8 +246,13 @@ int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
     L.demod = d_demod;
     L.demod_stride = demod_stride;
     L.demod_hist = demod_hist;
-    // the mono product's audio history stays in step with the stream (split-API use)
-    L.demod_tail = (c->geo.audio_up == 1) ? c->d_audio_hist.p : nullptr;
+    // When this call produces the mono audio itself, the mono product's audio history stays in
+    // step with the stream, so a later fmrx_audio_block continues from it: its last 50 samples
+    // are all a resampler output reads back (51 taps per phase in every mode).  The RF-only
+    // calls (fmrx_rf_block, the stereo engine) leave it alone: the audio stage they feed owns it.
+    L.demod_tail = with_audio ? c->d_audio_hist.p + (c->audio_hist - kAudioHist50) : nullptr;
+    L.demod_tail_stride = (size_t)c->audio_hist;
+    L.audio_coeff = c->d_audio.p;
     L.stream_bytes = n_blocks * c->geo.block_bytes;
     L.halo_bytes = c->halo_bytes;
     L.n_if = (long long)(n_blocks * c->geo.if_samples);
@@ -263,7 +270,8 @@ int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
         ev = &c->evs[c->ev_used++];
         HIPCHK(hipEventRecord(ev->first, c->stream));
     }
-    int rc = launch_mono_fused(L, ns, c->geo.rf_taps, c->geo.rf_decim, ad, c->mono_taps, c->stream);
+    int rc = launch_mono_fused(L, ns, c->geo.rf_taps, c->geo.rf_decim, c->geo.audio_up,
+                               c->geo.audio_up == 1 ? ad : c->geo.audio_down, c->mono_taps, c->stream);
     if (rc != 0) return fail(rc == -1 ? FMRX_EINVAL : FMRX_EHIP, "fused kernel launch failed (%d)", rc);
     if (ev) HIPCHK(hipEventRecord(ev->second, c->stream));
     rc = launch_halo_update(d_iq, L.stream_bytes, c->d_halo[c->halo_cur].p,
@@ -286,8 +294,8 @@ int run_mono_audio(fmrx_ctx* c, const float* d_demod, size_t demod_stride, size_
         const float* in = d_demod + s * demod_stride;
         float* st = c->d_audio_hist.p + (size_t)s * c->audio_hist;
         float* out = d_mono ? d_mono + s * na : c->d_scratch.p + s * na;
-        rc = launch_resample(out, st, in, (int)n_if, c->d_audio.p, at, c->geo.audio_up,
-                             c->geo.audio_down, (int)na, c->stream);
+        rc = launch_polyphase(out, st, in, c->d_audio.p, at, c->geo.audio_up, c->geo.audio_down, (int)na,
+                              c->stream);
         if (rc == 0) rc = launch_tail_copy(st, in + (n_if - (at - 1)), at - 1, c->stream);
         if (rc == 0) rc = launch_quantize(out, na, d_pcm + s * na, c->stream);
         if (rc) return fail(FMRX_EHIP, "mono audio stage launch failed");
@@ -582,14 +590,8 @@ int fmrx_process_device_ex(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, in
     int rc = set_device(c);
     if (rc) return rc;
     const size_t n_if = n_blocks * c->geo.if_samples;
-    if (c->cfg.channels == FMRX_MONO && c->geo.audio_up == 1)
+    if (c->cfg.channels == FMRX_MONO)  // every mode: RF + demod + audio resampler in one launch
         return run_fused(c, d_iq, n_blocks, d_pcm, d_mono, nullptr, 0, 0, true);
-    if (c->cfg.channels == FMRX_MONO) {
-        // modes 2/3: fused RF -> demod buffer, then the polyphase audio stage
-        if ((rc = c->d_f32.ensure(n_if * c->cfg.n_streams))) return rc;
-        if ((rc = run_fused(c, d_iq, n_blocks, nullptr, nullptr, c->d_f32.p, n_if, 0, false))) return rc;
-        return run_mono_audio(c, c->d_f32.p, n_if, n_if, d_pcm, d_mono);
-    }
     if ((rc = ensure_demod(c, n_if))) return rc;
     if ((rc = run_fused(c, d_iq, n_blocks, nullptr, nullptr, c->d_demod.p, c->demod_stride,
                         kDemodHist, false)))

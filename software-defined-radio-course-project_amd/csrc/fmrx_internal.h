@@ -40,7 +40,10 @@ struct MonoLaunch {
                                 //   demod_hist + g] for IF index g (stereo engine input)
     size_t demod_stride;
     int demod_hist;
-    float* demod_tail;          // optional: last audio_taps-1 demod samples, n_streams x AH
+    float* demod_tail;          // optional: the last AH demod samples, at demod_tail +
+                                //   s * demod_tail_stride for stream s
+    size_t demod_tail_stride;
+    const float* audio_coeff;   // modes 2/3: the rational resampler's prototype (device)
     size_t stream_bytes;        // n_blocks * block_bytes
     size_t halo_bytes;
     long long n_if;             // IF samples per stream this call
@@ -56,7 +59,7 @@ long long mono_chunks(long long n_if, int rf_taps, int rf_decim, int audio_down)
 int mono_wg_per_cu(int rf_decim);
 // Returns 0 on success, FMRX_EINVAL if no compiled variant matches.
 int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_decim,
-                      int audio_down, const MonoTaps& taps, hipStream_t s);
+                      int audio_up, int audio_down, const MonoTaps& taps, hipStream_t s);
 // Halo bookkeeping: new_halo = last halo_bytes of (old_halo ++ iq), per stream.
 int launch_halo_update(const uint8_t* iq, size_t stream_bytes, const uint8_t* old_halo,
                        uint8_t* new_halo, size_t halo_bytes, int n_streams, hipStream_t s);
@@ -125,6 +128,8 @@ int launch_psd(const float* x, int nseg, int N, const float* hann, double scale,
 // ---- generic filter.h primitives ------------------------------------------------------
 int launch_resample(float* out, const float* state, const float* in, int n_in,
                     const float* coeff, int taps, int up, int down, int n_out, hipStream_t s);
+int launch_polyphase(float* out, const float* state, const float* in, const float* coeff, int taps, int up,
+                     int down, int n_out, hipStream_t s);
 int launch_tail_copy(float* dst, const float* src, int n, hipStream_t s);
 int launch_fm_demod(float* out, float* prev, const float* i, const float* q, int n,
                     hipStream_t s);

@@ -104,12 +104,15 @@ __device__ inline float sbyte(uint32_t w) {
 // Measured and dropped: prefetching two chunks ahead, the audio stage once per
 // two chunks in packed ops, a single-buffered demod window with R = 2 for three waves per
 // SIMD, the audio FIR pipelined into the RF tap loop, staggered workgroup starts.
-template <int T, int D, int AD, int NT, int R, int PD, int ABL = 0, int TR = 0>
+// AU > 1: the audio stage is the rational resampler of modes 2/3 (up AU, down AD; 51 taps
+// per output phase of a 51*AU-tap prototype read from L.audio_coeff).
+template <int T, int D, int AD, int NT, int R, int PD, int ABL = 0, int TR = 0, int AU = 1>
 __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps taps) {
     using C = MonoCfg<T, D, AD, NT, R>;
     constexpr int CIF = C::CIF, P = C::P, H = C::H, S = C::S, G = C::G, NLD = C::NLD;
     constexpr int WH = C::WH, NG = C::NG;
     constexpr bool kShfl = NT == 64;
+    static_assert(AU == 1 || ((long long)CIF * AU + AD - 1) / AD + 1 <= NT, "one audio output per thread");
 
     __shared__ float4 xb4[C::XB / 2 + 1];        // scaled (I,Q) pairs, two per float4
     __shared__ float dbuf[2][kAH + CIF];         // demod window: 50 history + chunk
@@ -130,7 +133,7 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     const int c_full = (int)(L.stream_bytes / (2 * P));  // chunks lying wholly in the data
     const int c_tail = n_if >= kAH ? (int)((n_if - kAH) / CIF) : -2;  // chunks holding the last 50
     if (c0 >= c1) return;
-    const long long n_audio = n_if / AD;
+    const long long n_audio = n_if * AU / AD;
 
     const uint8_t* in = L.iq + (size_t)stream * L.stream_bytes;
     const uint8_t* halo = L.halo + (size_t)stream * L.halo_bytes;
@@ -316,7 +319,7 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                     if (L.demod)
                         L.demod[(size_t)stream * L.demod_stride + L.demod_hist + g] = d[r];
                     if (L.demod_tail && g >= n_if - kAH)
-                        L.demod_tail[(size_t)stream * kAH + (g - (n_if - kAH))] = d[r];
+                        L.demod_tail[(size_t)stream * L.demod_tail_stride + (g - (n_if - kAH))] = d[r];
                 }
             }
         }
@@ -325,7 +328,33 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         // ---- audio LPF + decimate + quantise: outputs m with AD*m in this chunk.  Chunk c
         // starts at IF index pos = c CIF = AD aq + ar (tracked incrementally); its first audio
         // output is m0 = aq + (ar > 0), at chunk offset off0 = AD m0 - pos.
-        if (L.audio && c >= c0) {
+        if constexpr (AU > 1) {
+            // rational resampler (project.cpp:146 with up = AU, down = AD): output m has phase
+            // k0 = (m AD) mod AU and base j0 = floor(m AD / AU); it reads demod j0 - i, i < 51,
+            // against coeff[k0 + i AU] (i ascending = k ascending, filter.cpp:84-92), and
+            // belongs to the chunk that holds j0 (its 50 predecessors are the window history)
+            if (L.audio && c >= c0) {
+                const long long mlo = ((long long)c * CIF * AU + AD - 1) / AD;
+                const long long mhi = ((long long)(c + 1) * CIF * AU + AD - 1) / AD;
+                const long long m = mlo + tid;
+                if (m < mhi && m < n_audio) {
+                    const long long nd = m * AD;
+                    const long long j0 = nd / AU;
+                    const int k0 = (int)(nd - j0 * AU);
+                    const float* dw = &dbuf[cur][kAH + (int)(j0 - (long long)c * CIF)];
+                    const float* cf = L.audio_coeff + k0;
+                    float a = 0.0f;
+#pragma unroll
+                    for (int i = 0; i < kAudioTaps; i++) {
+                        const float p = cf[i * AU] * dw[-i];
+                        a = a + p;
+                    }
+                    const size_t oi = (size_t)stream * (size_t)n_audio + (size_t)m;
+                    L.pcm[oi] = quantize_s16(a);
+                    if (L.mono) L.mono[oi] = a;
+                }
+            }
+        } else if (L.audio && c >= c0) {
             const int off0 = ar > 0 ? AD - ar : 0;
             const long long m0 = aq + (ar > 0);
             const long long left = n_audio - m0;  // outputs of the stream not yet written
@@ -350,9 +379,9 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     }
 }
 
-template <int T, int D, int AD, int NT, int R, int PD, int TR = 0>
+template <int T, int D, int AD, int NT, int R, int PD, int TR = 0, int AU = 1>
 int launch_variant(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStream_t s) {
-    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD, 0, TR>), dim3(n_streams * L.segs), dim3(NT), 0,
+    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD, 0, TR, AU>), dim3(n_streams * L.segs), dim3(NT), 0,
                        s, L, taps);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
@@ -408,8 +437,22 @@ int launch_ablation(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hi
 }
 
 int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_decim,
-                      int audio_down, const MonoTaps& taps, hipStream_t s) {
+                      int audio_up, int audio_down, const MonoTaps& taps, hipStream_t s) {
     const int vi = variant_index();
+    if (audio_up > 1 && L.audio) {
+        // modes 2/3 with the rational resampler fused (the default kernel shape; mode 3's odd
+        // decimation keeps R = 2)
+        if (rf_decim == 10 && audio_up == 147 && audio_down == 800) {
+            if (rf_taps == 51) return launch_variant<51, 10, 800, 64, 3, 4, 1, 147>(L, n_streams, taps, s);
+            if (rf_taps == 101) return launch_variant<101, 10, 800, 64, 3, 4, 1, 147>(L, n_streams, taps, s);
+        }
+        if (rf_decim == 9 && audio_up == 441 && audio_down == 2560) {
+            if (rf_taps == 51) return launch_variant<51, 9, 2560, 64, 2, 3, 0, 441>(L, n_streams, taps, s);
+            if (rf_taps == 101) return launch_variant<101, 9, 2560, 64, 2, 3, 0, 441>(L, n_streams, taps, s);
+        }
+        return -1;
+    }
+    if (audio_up > 1) audio_down = 5;  // RF + demod only (stereo engine, split API): any compiled AD
     if (const int a = ablation(); a != 0 && rf_taps == 101 && rf_decim == 10) {
         switch (a) {
             case 1: return launch_ablation<1>(L, n_streams, taps, s);

@@ -32,6 +32,48 @@ __global__ void resample_kernel(float* __restrict__ out, const float* __restrict
     out[n] = acc;
 }
 
+// The same resample for the rational audio resamplers (project.cpp:146; 147/800 and
+// 441/2560 in modes 2/3): output n has phase k0 = (n down) mod up and base input j0 =
+// floor(n down / up); its taps are coeff[k0 + i up] against in[j0 - i], i ascending (= k
+// ascending, as filter.cpp:84-92).  One division per output instead of one per tap; the
+// prototype keeps its order, so at tap step i a wave's lanes read inside one up-wide window.
+__global__ void polyphase_kernel(float* __restrict__ out, const float* __restrict__ state,
+                                 const float* __restrict__ in, const float* __restrict__ coeff,
+                                 int taps, int up, int down, int n_out) {
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_out) return;
+    const long long nd = (long long)n * down;
+    const long long j0 = nd / up;
+    const int k0 = (int)(nd - j0 * up);
+    const int cnt = (taps - k0 + up - 1) / up;  // taps of this phase: k0 + i up < taps
+    const float* c = coeff + k0;
+    float acc = 0.0f;
+    if (cnt == 51 && j0 >= 50) {
+        // every phase of the modes 2/3 prototypes (7497 = 51 x 147, 22491 = 51 x 441): a
+        // fixed trip count unrolls, so all 102 loads are in flight before the sum starts
+        const float* x = in + j0;
+#pragma unroll
+        for (int i = 0; i < 51; i++) {
+            const float p = c[i * up] * x[-i];
+            acc = acc + p;
+        }
+    } else if (j0 >= cnt - 1) {  // the whole window lies in this call's input
+        const float* x = in + j0;
+        for (int i = 0; i < cnt; i++) {
+            const float p = c[i * up] * x[-i];
+            acc = acc + p;
+        }
+    } else {
+        for (int i = 0; i < cnt; i++) {
+            const long long j = j0 - i;
+            const float x = j >= 0 ? in[j] : state[(taps - 1) + j];
+            const float p = c[i * up] * x;
+            acc = acc + p;
+        }
+    }
+    out[n] = acc;
+}
+
 __global__ void copy_kernel(float* __restrict__ dst, const float* __restrict__ src, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) dst[i] = src[i];
@@ -124,6 +166,14 @@ int launch_resample(float* out, const float* state, const float* in, int n_in,
     if (n_out <= 0) return 0;
     hipLaunchKernelGGL(resample_kernel, dim3(blocks_for(n_out, 256)), dim3(256), 0, s, out, state,
                        in, coeff, taps, up, down, n_out);
+    return ok();
+}
+
+int launch_polyphase(float* out, const float* state, const float* in, const float* coeff, int taps, int up,
+                     int down, int n_out, hipStream_t s) {
+    if (n_out <= 0) return 0;
+    hipLaunchKernelGGL(polyphase_kernel, dim3(blocks_for(n_out, 256)), dim3(256), 0, s, out, state, in, coeff,
+                       taps, up, down, n_out);
     return ok();
 }
 

@@ -161,16 +161,36 @@ __device__ inline float mixer_at(const AudioView& v, int i) { return 2.0f * (v.c
 
 // mono of block b, frame m (project.cpp:146): history = previous block's mixer tail
 // (or the carried tail for the first block of a call).
+// Output m of the resampler: phase k0 = (m down) mod up, base input j0 = floor(m down / up);
+// taps k = k0 + i up (i ascending = k ascending, filter.cpp:84-92) against input j0 - i: one
+// division per output, none per tap.  The prototype stays in its own order: at tap step i the
+// lanes of a wave read inside one up-wide window (coalesced), where a phase-major table would
+// scatter them over up rows.
+struct Phase {
+    long long j0;
+    const float* c;  // c[i * up] = coeff[k0 + i up]
+    int cnt;
+};
+__device__ inline Phase phase_of(const AudioLaunch& L, int m) {
+    const long long nd = (long long)m * L.down;
+    Phase p;
+    p.j0 = nd / L.up;
+    const int k0 = (int)(nd - p.j0 * L.up);
+    p.cnt = (L.at - k0 + L.up - 1) / L.up;
+    p.c = L.audio_c + k0;
+    return p;
+}
+
 __device__ inline float mono_at(const AudioLaunch& L, const AudioView& cur, const AudioView& prv,
                                 bool has_prev, const float* tail, int tl, int m) {
-    const long long nd = (long long)m * L.down;
+    const Phase ph = phase_of(L, m);
     float acc = 0.0f;
-    for (int k = (int)(nd % L.up); k < L.at; k += L.up) {
-        const long long j = (nd - k) / L.up;
+    for (int i = 0; i < ph.cnt; i++) {
+        const long long j = ph.j0 - i;
         float x;
         if (j >= 0) x = cur.d[j];
         else x = has_prev ? mixer_at(prv, L.if_per_block + (int)j) : tail[tl + j];
-        const float p = L.audio_c[k] * x;
+        const float p = ph.c[i * L.up] * x;
         acc = acc + p;
     }
     return acc;
@@ -178,12 +198,12 @@ __device__ inline float mono_at(const AudioLaunch& L, const AudioView& cur, cons
 
 // stereo of block b, frame m (project.cpp:172): history = the same block's demod tail.
 __device__ inline float stereo_at(const AudioLaunch& L, const AudioView& cur, int m) {
-    const long long nd = (long long)m * L.down;
+    const Phase ph = phase_of(L, m);
     float acc = 0.0f;
-    for (int k = (int)(nd % L.up); k < L.at; k += L.up) {
-        const long long j = (nd - k) / L.up;
+    for (int i = 0; i < ph.cnt; i++) {
+        const long long j = ph.j0 - i;
         const float x = j >= 0 ? mixer_at(cur, (int)j) : cur.d[L.if_per_block + j];
-        const float p = L.audio_c[k] * x;
+        const float p = ph.c[i * L.up] * x;
         acc = acc + p;
     }
     return acc;

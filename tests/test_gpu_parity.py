@@ -114,6 +114,44 @@ def test_mono_call_split_and_resume(fmrx, orc, mode, rf_taps):
         assert np.array_equal(np.concatenate(parts), want)
 
 
+@pytest.mark.parametrize("mode,nb", [(2, 6), (3, 4)])
+def test_polyphase_mono_split_resume_and_mixed_api(fmrx, orc, mode, nb):
+    """Modes 2/3 run the rational resampler inside the fused kernel; its history must survive
+    call splits, a checkpoint into a second context, and hand-over to the split API."""
+    bb, rf_fs = oracle.MODES[mode][0], oracle.MODES[mode][3]
+    iq = iqgen.make("synth:61", nb * bb, rf_fs)
+    want = orc.run(mode, 51, iq, ["pcm_mono"])["pcm_mono"]
+    na = oracle.MODES[mode][2]
+    with fmrx.Receiver(mode, fmrx.MONO) as rx:
+        parts, pos = [], 0
+        for n in (1, 2, nb - 3):
+            parts.append(rx.process(iq[pos * bb:(pos + n) * bb]))
+            pos += n
+            if pos == 1:
+                with fmrx.Receiver(mode, fmrx.MONO) as rx2:
+                    rx2.set_state(rx.get_state())
+                    assert np.array_equal(rx2.process(iq[bb:]), want[na:])
+        assert np.array_equal(np.concatenate(parts), want)
+        rx.reset()
+        first = rx.process(iq[:2 * bb])  # fused ...
+        rest = rx.audio_block(rx.rf_block(iq[2 * bb:]))  # ... then the reference's thread split
+        assert np.array_equal(np.concatenate([first, rest]), want)
+
+
+@pytest.mark.parametrize("mode,nb", [(0, 7), (1, 5), (2, 3)])
+def test_thread_split_block_by_block(fmrx, orc, mode, nb):
+    """project.cpp's thread split on one context, block by block: rf_block(b) then
+    audio_block(b) (the audio stage owns the audio history, the RF stage must not touch it)."""
+    bb, rf_fs = oracle.MODES[mode][0], oracle.MODES[mode][3]
+    iq = iqgen.make("synth:62", nb * bb, rf_fs)
+    with fmrx.Receiver(mode, fmrx.MONO) as rx:
+        got = [rx.audio_block(rx.rf_block(iq[b * bb:(b + 1) * bb])) for b in range(nb)]
+    assert np.array_equal(np.concatenate(got), orc.run(mode, 51, iq, ["pcm_mono"])["pcm_mono"])
+    with fmrx.Receiver(mode, fmrx.STEREO) as rx:
+        got = [rx.audio_block(rx.rf_block(iq[b * bb:(b + 1) * bb])) for b in range(nb)]
+    assert np.array_equal(np.concatenate(got), orc.run(mode, 51, iq, ["pcm"])["pcm"])
+
+
 def test_mono_multistream_independent(fmrx, orc):
     nb, bb = 23, 12800
     ins = [iqgen.make(r, nb * bb) for r in ("synth:51", "rand:52", "synth:53", "const128")]
