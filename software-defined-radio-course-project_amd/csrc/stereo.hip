@@ -109,26 +109,36 @@ __global__ void pll_kernel(float* io, int n, int n_streams, size_t stride, float
     const double step = (2.0 * kPi) * static_cast<double>(freq / fs);
     int i = 0;
     if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
-        // batches of 16 with the next batch in flight while this one runs
-        float4 cur[4], nxt[4];
+        // Batches of 16 samples in two register sets used alternately (A: even batches, B:
+        // odd), each loaded a whole batch before its use: with one set copied forward the
+        // compiler waits for the next batch's loads (and the stores) at the top of every
+        // batch, exposing a memory round trip per 16 steps.
+        float4 A[4], B[4];
         const int nb = n / kPllBatch;
-        if (nb > 0)
-            for (int q = 0; q < 4; q++) cur[q] = reinterpret_cast<const float4*>(x)[q];
-        for (int b = 0; b < nb; b++) {
-            if (b + 1 < nb)
-                for (int q = 0; q < 4; q++)
-                    nxt[q] = reinterpret_cast<const float4*>(x + (b + 1) * kPllBatch)[q];
-            float4 out[4];
+        auto load = [&](float4 (&dst)[4], int b) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) dst[q] = reinterpret_cast<const float4*>(x + b * kPllBatch)[q];
+        };
+        auto run = [&](float4 (&src)[4], int b) {
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                out[q].x = pll_step(p, ctx, cur[q].x, Ki, Kp, step, lib);
-                out[q].y = pll_step(p, ctx, cur[q].y, Ki, Kp, step, lib);
-                out[q].z = pll_step(p, ctx, cur[q].z, Ki, Kp, step, lib);
-                out[q].w = pll_step(p, ctx, cur[q].w, Ki, Kp, step, lib);
+                float4 o;
+                o.x = pll_step(p, ctx, src[q].x, Ki, Kp, step, lib);
+                o.y = pll_step(p, ctx, src[q].y, Ki, Kp, step, lib);
+                o.z = pll_step(p, ctx, src[q].z, Ki, Kp, step, lib);
+                o.w = pll_step(p, ctx, src[q].w, Ki, Kp, step, lib);
+                reinterpret_cast<float4*>(x + b * kPllBatch)[q] = o;
             }
-            for (int q = 0; q < 4; q++) reinterpret_cast<float4*>(x + b * kPllBatch)[q] = out[q];
-            for (int q = 0; q < 4; q++) cur[q] = nxt[q];
+        };
+        if (nb > 0) load(A, 0);
+        int b = 0;
+        for (; b + 1 < nb; b += 2) {
+            load(B, b + 1);
+            run(A, b);
+            if (b + 2 < nb) load(A, b + 2);
+            run(B, b + 1);
         }
+        if (b < nb) run(A, b);
         i = nb * kPllBatch;
     }
     for (; i < n; i++) x[i] = pll_step(p, ctx, x[i], Ki, Kp, step, lib);
