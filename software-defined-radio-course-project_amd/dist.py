@@ -33,8 +33,10 @@ def gather_pcm(local: torch.Tensor, n_streams: int, pcm_len: int, world: int, ra
     max_local = len(shard(n_streams, world, 0))
     send = torch.zeros((max_local, pcm_len), dtype=local.dtype, device=local.device)
     send[: local.shape[0]] = local
-    # RCCL/NCCL and gloo have no int16 type: move the PCM as raw bytes.
+    # RCCL/NCCL and gloo have no int16 type: move the PCM as raw bytes (gloo: host memory).
     send8 = send.view(torch.uint8)
+    if dist.get_backend() == "gloo" and send8.is_cuda:
+        send8 = send8.cpu()
     bufs = [torch.empty_like(send8) for _ in range(world)] if rank == dst else None
     dist.gather(send8, bufs, dst=dst)
     if rank != dst:
