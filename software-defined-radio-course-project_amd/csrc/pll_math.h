@@ -242,4 +242,26 @@ FMRX_HD float pll_step(PllState& p, PllCtx& ctx, float v, float Ki, float Kp, do
     return arg;
 }
 
+// The same step on the certified fast paths only: no library fallback, no branch.  Every
+// certification flag is ANDed into `ok`; when it ends false the step's results (and those of
+// any later step computed from them) are not to be used -- the caller restores the state and
+// redoes the steps with pll_step.  When `ok` stays true the results equal pll_step's exactly
+// (the same arithmetic), so a straight-line run of many steps can be validated at once.
+FMRX_HD float pll_step_fast(PllState& p, PllCtx& ctx, float v, float Ki, float Kp, double step, int& ok) {
+    const float eI = v * p.fbI;
+    const float eQ = v * (-p.fbQ);
+    float e;
+    ok &= (int)rot_atan2_f(eQ, eI, ctx, &e);
+    p.integ = p.integ + Ki * e;
+    p.phase = p.phase + ((Kp * e) + p.integ);
+    p.trig = p.trig + 1.0f;
+    const double prod = step * (double)p.trig;
+    const float arg = (float)(prod + (double)p.phase);
+    float sv, cv;
+    ok &= (int)sincos_ctx_f(arg, &sv, &cv, &ctx);
+    p.fbI = cv;
+    p.fbQ = sv;
+    return arg;
+}
+
 }  // namespace fmrx

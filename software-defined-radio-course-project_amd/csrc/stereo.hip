@@ -70,7 +70,7 @@ __global__ void bpf_pair_generic(StereoLaunch L, BpTaps t) {
 // The recurrence only needs atan2 and sincos; the NCO output cos(trigArg * ncoScale +
 // phaseAdjust) (filter.cpp:170) depends on nothing later, so the serial loop stores trigArg
 // in place and pll_nco_kernel evaluates the NCO for all samples in parallel afterwards.
-// Full-precision fallbacks (HIP's double atan2/sin/cos), out of line: taken ~1e-7 of calls.
+// Full-precision fallbacks (HIP's double atan2/sin/cos), out of line: taken ~1e-6 of steps.
 __device__ __noinline__ float atan2_lib(float y, float x) {
     float e;
     if (fast_atan2_f(y, x, &e)) return e;
@@ -92,7 +92,7 @@ struct DeviceLib {
 
 constexpr int kPllBatch = 16;  // samples prefetched per batch (4 x 16-B loads)
 
-__global__ void pll_kernel(float* io, int n, int n_streams, size_t stride, float freq, float fs,
+__global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams, size_t stride, float freq, float fs,
                            float norm_bw, float* st) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_streams) return;
@@ -119,15 +119,38 @@ __global__ void pll_kernel(float* io, int n, int n_streams, size_t stride, float
 #pragma unroll
             for (int q = 0; q < 4; q++) dst[q] = reinterpret_cast<const float4*>(x + b * kPllBatch)[q];
         };
+        // Optimistic batches: the 16 steps run straight-line on the certified fast paths (no
+        // per-step branch, so the compiler schedules across steps); only if some step of this
+        // stream could not be certified (~1e-4 per step) is the batch redone from the saved
+        // state on the exact path with the library fallbacks.  Bit-identical either way.
         auto run = [&](float4 (&src)[4], int b) {
+            const PllState p0 = p;
+            const PllCtx ctx0 = ctx;
+            float4 o[4];
+            int ok = 1;
+            // (`ok` is forced into a VGPR after every step: left as an i1 the compiler keeps
+            // every certification mask of the batch live in SGPR pairs until the final AND
+            // and spills ~800 of them)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                float4 o;
-                o.x = pll_step(p, ctx, src[q].x, Ki, Kp, step, lib);
-                o.y = pll_step(p, ctx, src[q].y, Ki, Kp, step, lib);
-                o.z = pll_step(p, ctx, src[q].z, Ki, Kp, step, lib);
-                o.w = pll_step(p, ctx, src[q].w, Ki, Kp, step, lib);
-                reinterpret_cast<float4*>(x + b * kPllBatch)[q] = o;
+                o[q].x = pll_step_fast(p, ctx, src[q].x, Ki, Kp, step, ok);
+                asm volatile("" : "+v"(ok));
+                o[q].y = pll_step_fast(p, ctx, src[q].y, Ki, Kp, step, ok);
+                asm volatile("" : "+v"(ok));
+                o[q].z = pll_step_fast(p, ctx, src[q].z, Ki, Kp, step, ok);
+                asm volatile("" : "+v"(ok));
+                o[q].w = pll_step_fast(p, ctx, src[q].w, Ki, Kp, step, ok);
+                asm volatile("" : "+v"(ok));
+            }
+            if (!ok) {  // rare: redo from the saved state on the exact path
+                p = p0;
+                ctx = ctx0;
+                float* xb = x + b * kPllBatch;
+#pragma unroll 1
+                for (int j = 0; j < kPllBatch; j++) xb[j] = pll_step(p, ctx, xb[j], Ki, Kp, step, lib);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; q++) reinterpret_cast<float4*>(x + b * kPllBatch)[q] = o[q];
             }
         };
         if (nb > 0) load(A, 0);
