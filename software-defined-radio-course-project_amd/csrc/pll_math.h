@@ -136,84 +136,120 @@ FMRX_HD bool fast_atan2_f(float yf, float xf, float* out) {
     return decide_float(a, 3.0e-15 * fabs(a), out);
 }
 
-// ---- the PLL step (src/filter.cpp:157-171) with a short dependency chain ----------------
+// ---- the PLL step (src/filter.cpp:157-171) ---------------------------------------------
 //
-// The phase error e = atan2(eQ, eI) with (eI, eQ) = v * (fbI, -fbQ), fbI/fbQ = float(cos/sin
-// of the previous trigArg phi).  The previous step's sincos left cos(phi), sin(phi) in DOUBLE
-// (C, S) and phi's reduction phi = r + q*pi/2 (mod 2 pi).  Rotating (eI, eQ) by +phi gives
-// (X, Y) with angle theta + phi = a tiny residual d (float roundings only, |d| < 1e-6) or
-// pi + d when v < 0, hence  theta = atan(Y/X) + [X<0] pi - r - q pi/2  (mod 2 pi),  with
-// atan(Y/X) = Y/X to 1e-18 at that size.  Absolute error budget: (C, S) angle 1.5e-15,
-// rotation 3e-16, r 1e-16, constants 2e-16, glibc 1 ulp(pi) 4.4e-16 -> E = 4e-15, certified
-// by decide_float like the kernels above; anything else takes the generic path.
+// Per sample the reference computes, in float with double libm calls:
+//   eI = v fbI;  eQ = v (-fbQ);  e = float(atan2(eQ, eI));
+//   integ += Ki e;  phase += Kp e + integ;  trig += 1;
+//   x = float(step trig + phase);  fbI = float(cos x);  fbQ = float(sin x).
+//
+// Representation.  The sincos of x reduces x = r + nd pi/2 (|r| <= pi/4, q = nd mod 4) and
+// evaluates cs = cos r, sn = sin r in double; (fbI, fbQ) is the quadrant permutation (with
+// signs) of (float(cs), float(sn)), since float rounding commutes with both.  Undoing that
+// permutation on the next step's products gives, exactly,
+//     (a, b) := i^q (eI + i eQ) = (fl(v fc), fl(v nfs)),   fc = float(cs), nfs = -float(sn),
+// and rotating (a, b) by r in double gives (X, Y) = v (1 + O(2^-23), O(2^-23)), so
+//     theta = atan2(eQ, eI) = d + pi [v < 0] - x  (mod 2 pi),   d = atan(Y / X) ~ Y / X.
+// B = wrap(pi [v < 0] - x) follows from x alone by a Cody-Waite reduction, so theta = d + B
+// is one add on the recurrence's dependency chain and the loop carries no quadrant work.
+//
+// Error of th = d + B (absolute): (cs, sn) angle <= 1.5e-15 (their relative bound), X/Y
+// roundings 1e-16, r 1e-16, B's two roundings 4.4e-16, the add 2.2e-16, atan(d) - d <= 1.5e-16
+// (|d| < 2^-17), glibc's own <= 1 ulp(pi) 4.4e-16: <= 3.2e-15 < E = 4e-15.  e = float(th) is
+// certified when th - E and th + E round to the same float; |B| <= pi - 2^-12 keeps th off
+// atan2's branch cut.  sin/cos keep the fdlibm relative bound (the 16-ulp test above).
+
+constexpr double kInv2Pi = 1.59154943091895345608e-01;  // 1 / (2 pi)
+constexpr double kPllE = 4.0e-15;                       // absolute error bound of th
+constexpr double kPllMaxD = 0x1p-17;                    // |d|: atan(d) = d to 1.5e-16
+constexpr double kPiHi = 3.14159265358979311600e+00;
+constexpr double kPllMaxB = kPiHi - 0x1p-12;            // |B|: off the branch cut
+constexpr double kPllMinR = 0x1p-20;                    // |r|: sin r not tiny
+constexpr double kPllMaxX = 1.0e9;                      // |x|: reduction exact enough
+constexpr float kPllMinV = 0x1p-100f;                   // |v|: products stay normal
 
 struct PllCtx {
-    double C, S, r;  // cos/sin(phi) and phi's reduced argument from the last sincos
-    int q;           // phi's quadrant, phi = r + q*pi/2 (mod 2 pi)
-    bool valid;
+    double cs, sn;  // cos r, sin r of the last trigArg x = r + nd pi/2
+    double x;       // that trigArg (a float, exact in double)
+    int q;          // nd mod 4
+    bool valid;     // fields set and |x| < kPllMaxX
 };
 
-constexpr double kPiHi = 3.14159265358979311600e+00;
-
-FMRX_HD bool rot_atan2_f(float eQ, float eI, const PllCtx& c, float* out) {
-    // Branch-free: every test folds into one predicate (the PLL runs one lane per stream,
-    // where each taken-or-not branch costs as much as several arithmetic ops).
-    const double ei = (double)eI, eq = (double)eQ;
-    const double X = fma(ei, c.C, -(eq * c.S));
-    const double Y = fma(ei, c.S, eq * c.C);
-    // 1/X: hardware reciprocal estimate + one Newton step (relative error ~2^-52; |d| < 1e-4
-    // makes its contribution < 1e-20 absolute)
-#ifdef __HIP_DEVICE_COMPILE__
-    const double y0 = __builtin_amdgcn_rcp(X);
-#else
-    const double y0 = 1.0 / X;
-#endif
-    const double y1 = fma(y0, fma(-X, y0, 1.0), y0);
-    const double d = Y * y1;
-    const int k = ((X < 0.0 ? 2 : 0) - c.q) & 3;
-    const double kd = (double)k;
-    const double t0 = fma(kd, kPio2Lo, fma(kd, kPio2Hi, d - c.r));
-    const double th = t0 > kPiHi ? (t0 - 2.0 * kPiHi) - 2.0 * kPiLo : t0;
-    const float lo = (float)(th - 4.0e-15), hi = (float)(th + 4.0e-15);
-    *out = (float)th;
-    // zeros (C99 signed-zero rules), residual too large, too close to the +-pi cut, or an
-    // uncertified rounding: generic path
-    return (int)c.valid & (int)(eI != 0.0f) & (int)(eQ != 0.0f) & (int)(fabs(d) < 1.0e-4) &
-           (int)(fabs(fabs(th) - kPiHi) > 1.0e-9) & (int)(lo == hi);
+// wrap(pi [v < 0] - x) into [-pi, pi]: m = rint(x / (2 pi) + [v < 0] / 2), J = 2m - [v < 0]
+// (exact), B = J pi - x with the exact product inside each fma.  hneg = 0.5 [v < 0].
+FMRX_HD double pll_offset(double x, double hneg) {
+    const double m = rint(fma(x, kInv2Pi, hneg));
+    const double J = 2.0 * (m - hneg);
+    return fma(J, kPiLo, fma(J, kPiHi, -x));
 }
 
-// sin/cos of a float argument with the context for the next rot_atan2_f.
+// Y / X for |Y / X| < 2^-17 to ~2^-46 relative: one reciprocal and one Newton step on the
+// device (a division costs a dozen dependent ops); the host divides.
+FMRX_HD double pll_quot(double Y, double X) {
+#ifdef __HIP_DEVICE_COMPILE__
+    const double y0 = __builtin_amdgcn_rcp(X);
+    return Y * fma(y0, fma(-X, y0, 1.0), y0);
+#else
+    return Y / X;
+#endif
+}
+
+// fdlibm's sin/cos kernels for |r| <= pi/4 in Estrin form (shorter dependency chain).
+FMRX_HD void pll_sincos_kernel(double r, double* sn, double* cs) {
+    const double z = r * r, z2 = z * z, z4 = z2 * z2;
+    const double ps = fma(z4, fma(z, kS6, kS5), fma(z2, fma(z, kS4, kS3), fma(z, kS2, kS1)));
+    *sn = fma(z * r, ps, r);
+    const double pc = fma(z4, fma(z, kC6, kC5), fma(z2, fma(z, kC4, kC3), fma(z, kC2, kC1)));
+    *cs = 1.0 - (0.5 * z - z2 * pc);
+}
+
+// decide_float_16ulp's margin as a number: > 32 iff the float rounding of v is certified
+// (the low 29 bits lie more than 16 ulps from the halfway point 2^28).
+FMRX_HD uint32_t pll_margin16(double v) {
+    return ((uint32_t)__builtin_bit_cast(uint64_t, v) & 0x1FFFFFFFu) - (0x10000000u - 16u);
+}
+
+// atan2(eQ, eI) rounded to float, from the context of the previous sincos.  Returns false
+// when the rounding cannot be certified (zeros and tiny products, a first step without a
+// context, near the branch cut): the caller falls back to the library.
+FMRX_HD bool rot_atan2_f(float eQ, float eI, const PllCtx& c, float* out) {
+    const float a0 = (c.q & 1) ? -eQ : eI, b0 = (c.q & 1) ? eI : eQ;  // (a, b) = i^q (eI + i eQ)
+    const float a = (c.q & 2) ? -a0 : a0, b = (c.q & 2) ? -b0 : b0;
+    const double ad = (double)a, bd = (double)b;
+    const double X = fma(ad, c.cs, -(bd * c.sn));
+    const double Y = fma(ad, c.sn, bd * c.cs);
+    const double d = pll_quot(Y, X);
+    const double B = pll_offset(c.x, X < 0.0 ? 0.5 : 0.0);
+    const double th = d + B;
+    const float lo = (float)(th - kPllE), hi = (float)(th + kPllE);
+    *out = lo;
+    return (int)c.valid & (int)(fabsf(eI) >= kPllMinV) & (int)(fabsf(eQ) >= kPllMinV) &
+           (int)(fabs(d) < kPllMaxD) & (int)(fabs(B) <= kPllMaxB) & (int)(lo == hi);
+}
+
+// sin/cos of a float argument rounded to float, leaving the context for the next
+// rot_atan2_f.  Returns false when the rounding cannot be certified (caller falls back);
+// the context is valid whenever |x| < kPllMaxX either way.
 FMRX_HD bool sincos_ctx_f(float xf, float* s_out, float* c_out, PllCtx* ctx) {
     const double x = (double)xf;
-    const bool in_range = (int)(fabs(x) < 1.0e9) & (int)(fabs(x) > 1.0e-30);  // rejects inf/nan/0
+    const bool in_range = fabs(x) < kPllMaxX;  // rejects inf / nan too
     const double nd = rint(in_range ? x * kInvPio2 : 0.0);
-    const double r1 = fma(-nd, kPio2Hi, x);
-    const double r = fma(-nd, kPio2Lo, r1);
-    const double z = r * r, z2 = z * z, z4 = z2 * z2;
-    // same fdlibm kernels in Estrin form (shorter dependency chain)
-    const double ps = fma(z4, fma(z, kS6, kS5), fma(z2, fma(z, kS4, kS3), fma(z, kS2, kS1)));
-    const double sn = fma(z * r, ps, r);
-    const double pc = fma(z4, fma(z, kC6, kC5), fma(z2, fma(z, kC4, kC3), fma(z, kC2, kC1)));
-    const double cs = 1.0 - (0.5 * z - (z * z) * pc);
+    const double r = fma(-nd, kPio2Lo, fma(-nd, kPio2Hi, x));
+    double sn, cs;
+    pll_sincos_kernel(r, &sn, &cs);
     const int q = (int)nd & 3;  // |nd| < 6.4e8 fits an int; & 3 is mod 4 for negatives too
-    const double sv = (q & 1) ? cs : sn, cv0 = (q & 1) ? sn : cs;
-    // quadrant signs as sign-bit flips (q & 2 for sin, (q + 1) & 2 for cos)
-    const double s2 = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, sv) ^ ((uint64_t)(q & 2) << 62));
-    const double c2 =
-        __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, cv0) ^ ((uint64_t)((q + 1) & 2) << 62));
-    // Certified rounding: relative error <= 1.5e-15 (13.5 ulp), and the absolute reduction
-    // term |nd| 1e-32 stays below 0.03 ulp for |v| >= 2^-20 -> a 16-ulp window; smaller
-    // results (probability ~1e-6 per call) take the library path.
-    const bool s_ok = (int)decide_float_16ulp(s2, s_out) & (int)(fabs(s2) >= 0x1p-20);
-    const bool c_ok = (int)decide_float_16ulp(c2, c_out) & (int)(fabs(c2) >= 0x1p-20);
-    // (C, S, r, q) are within the bounds rot_atan2_f assumes whether or not the float
-    // rounding could be certified here, so the context is valid either way.
-    ctx->C = c2;
-    ctx->S = s2;
-    ctx->r = r;
+    const float fs = (float)sn, fc = (float)cs;
+    // cos x = [cs, -sn, -cs, sn][q], sin x = [sn, cs, -sn, -cs][q]
+    const float c = (q & 1) ? fs : fc, s = (q & 1) ? fc : fs;
+    *c_out = ((q + 1) & 2) ? -c : c;
+    *s_out = (q & 2) ? -s : s;
+    ctx->cs = cs;
+    ctx->sn = sn;
+    ctx->x = x;
     ctx->q = q;
     ctx->valid = in_range;
-    return (int)in_range & (int)s_ok & (int)c_ok;
+    return (int)in_range & (int)(pll_margin16(sn) > 32u) & (int)(pll_margin16(cs) > 32u) &
+           (int)(fabs(r) >= kPllMinR);
 }
 
 struct PllState {
@@ -242,26 +278,74 @@ FMRX_HD float pll_step(PllState& p, PllCtx& ctx, float v, float Ki, float Kp, do
     return arg;
 }
 
-// The same step on the certified fast paths only: no library fallback, no branch.  Every
-// certification flag is ANDed into `ok`; when it ends false the step's results (and those of
-// any later step computed from them) are not to be used -- the caller restores the state and
-// redoes the steps with pll_step.  When `ok` stays true the results equal pll_step's exactly
-// (the same arithmetic), so a straight-line run of many steps can be validated at once.
-FMRX_HD float pll_step_fast(PllState& p, PllCtx& ctx, float v, float Ki, float Kp, double step, int& ok) {
-    const float eI = v * p.fbI;
-    const float eQ = v * (-p.fbQ);
-    float e;
-    ok &= (int)rot_atan2_f(eQ, eI, ctx, &e);
-    p.integ = p.integ + Ki * e;
-    p.phase = p.phase + ((Kp * e) + p.integ);
-    p.trig = p.trig + 1.0f;
-    const double prod = step * (double)p.trig;
-    const float arg = (float)(prod + (double)p.phase);
-    float sv, cv;
-    ok &= (int)sincos_ctx_f(arg, &sv, &cv, &ctx);
-    p.fbI = cv;
-    p.fbQ = sv;
-    return arg;
+// N steps straight-line on the certified fast paths, with no branch and no quadrant work
+// (the representation above): the loop carries (fc, nfs, cs, sn, B) and folds every
+// certification into a few accumulators checked once at the end.  Returns true when every
+// step was certified -- the outputs and (p, ctx) then equal N pll_step calls bit for bit.
+// Otherwise p and ctx are garbage: the caller restores them and redoes the N steps with
+// pll_step.  NaN anywhere reaches the phase accumulator and fails the final check.
+template <int N>
+FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], float (&out)[N], float Ki,
+                            float Kp, double step) {
+    // undo the quadrant permutation: fc = [fbI, fbQ, -fbI, -fbQ][q], nfs = [-fbQ, fbI, fbQ, -fbI][q]
+    const int q0 = ctx.q;
+    const float u0 = (q0 & 1) ? p.fbQ : p.fbI, w0 = (q0 & 1) ? p.fbI : -p.fbQ;
+    float fc = (q0 & 2) ? -u0 : u0, nfs = (q0 & 2) ? -w0 : w0;
+    double cs = ctx.cs, sn = ctx.sn, x = ctx.x, nd = 0.0;
+    double B = pll_offset(x, v[0] < 0.0f ? 0.5 : 0.0);
+    uint32_t acc_u = 0xFFFFFFFFu, acc_e = 0u;
+    double acc_d = 0.0, acc_B = fabs(B), acc_x = 0.0, acc_r = 1.0;
+    float acc_v = fabsf(v[0]);
+#ifdef __HIPCC__
+#pragma unroll
+#endif
+    for (int j = 0; j < N; j++) {
+        const float a = v[j] * fc, b = v[j] * nfs;
+        const double ad = (double)a, bd = (double)b;
+        const double X = fma(ad, cs, -(bd * sn));
+        const double Y = fma(ad, sn, bd * cs);
+        const double d = pll_quot(Y, X);
+        const double th = d + B;
+        const float lo = (float)(th - kPllE), hi = (float)(th + kPllE);
+        acc_e |= __builtin_bit_cast(uint32_t, lo) ^ __builtin_bit_cast(uint32_t, hi);
+        acc_d = fmax(acc_d, fabs(d));
+        const float e = lo;
+        p.integ = p.integ + Ki * e;
+        p.phase = p.phase + ((Kp * e) + p.integ);
+        p.trig = p.trig + 1.0f;
+        const float arg = (float)(step * (double)p.trig + (double)p.phase);
+        out[j] = arg;
+        x = (double)arg;
+        acc_x = fmax(acc_x, fabs(x));
+        nd = rint(x * kInvPio2);
+        const double r = fma(-nd, kPio2Lo, fma(-nd, kPio2Hi, x));
+        acc_r = fmin(acc_r, fabs(r));
+        pll_sincos_kernel(r, &sn, &cs);
+        fc = (float)cs;
+        nfs = -(float)sn;
+        const uint32_t mc = pll_margin16(cs), ms = pll_margin16(sn);
+        acc_u = acc_u < mc ? acc_u : mc;
+        acc_u = acc_u < ms ? acc_u : ms;
+        if (j + 1 < N) {
+            B = pll_offset(x, v[j + 1] < 0.0f ? 0.5 : 0.0);
+            acc_B = fmax(acc_B, fabs(B));
+            acc_v = fminf(acc_v, fabsf(v[j + 1]));
+        }
+    }
+    // the quadrant permutation back: fbI = [fc, nfs, -fc, -nfs][q], fbQ = [-nfs, fc, nfs, -fc][q]
+    const int q = (int)nd & 3;
+    const float c1 = (q & 1) ? nfs : fc, s1 = (q & 1) ? fc : -nfs;
+    p.fbI = (q & 2) ? -c1 : c1;
+    p.fbQ = (q & 2) ? -s1 : s1;
+    const bool valid0 = ctx.valid;
+    ctx.cs = cs;
+    ctx.sn = sn;
+    ctx.x = x;
+    ctx.q = q;
+    ctx.valid = true;
+    return (int)valid0 & (int)(acc_u > 32u) & (int)(acc_e == 0u) & (int)(acc_d < kPllMaxD) &
+           (int)(acc_B <= kPllMaxB) & (int)(acc_x < kPllMaxX) & (int)(acc_r >= kPllMinR) &
+           (int)(acc_v >= kPllMinV) & (int)(p.phase == p.phase);
 }
 
 }  // namespace fmrx

@@ -113,44 +113,31 @@ __global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams
         // odd), each loaded a whole batch before its use: with one set copied forward the
         // compiler waits for the next batch's loads (and the stores) at the top of every
         // batch, exposing a memory round trip per 16 steps.
-        float4 A[4], B[4];
+        float A[kPllBatch], B[kPllBatch];
         const int nb = n / kPllBatch;
-        auto load = [&](float4 (&dst)[4], int b) {
+        auto load = [&](float (&dst)[kPllBatch], int b) {
 #pragma unroll
-            for (int q = 0; q < 4; q++) dst[q] = reinterpret_cast<const float4*>(x + b * kPllBatch)[q];
+            for (int q = 0; q < kPllBatch / 4; q++)
+                *reinterpret_cast<float4*>(&dst[4 * q]) = reinterpret_cast<const float4*>(x + b * kPllBatch)[q];
         };
-        // Optimistic batches: the 16 steps run straight-line on the certified fast paths (no
-        // per-step branch, so the compiler schedules across steps); only if some step of this
-        // stream could not be certified (~1e-4 per step) is the batch redone from the saved
-        // state on the exact path with the library fallbacks.  Bit-identical either way.
-        auto run = [&](float4 (&src)[4], int b) {
+        // Optimistic batches: the 16 steps run straight-line on the certified fast paths
+        // (pll_batch_fast: no per-step branch, no quadrant bookkeeping); only if some step of
+        // this stream could not be certified (~1e-4 per step) is the batch redone from the
+        // saved state on the exact path with the library fallbacks.  Bit-identical either way.
+        auto run = [&](float (&src)[kPllBatch], int b) {
             const PllState p0 = p;
             const PllCtx ctx0 = ctx;
-            float4 o[4];
-            int ok = 1;
-            // (`ok` is forced into a VGPR after every step: left as an i1 the compiler keeps
-            // every certification mask of the batch live in SGPR pairs until the final AND
-            // and spills ~800 of them)
+            float o[kPllBatch];
+            if (pll_batch_fast(p, ctx, src, o, Ki, Kp, step)) {
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                o[q].x = pll_step_fast(p, ctx, src[q].x, Ki, Kp, step, ok);
-                asm volatile("" : "+v"(ok));
-                o[q].y = pll_step_fast(p, ctx, src[q].y, Ki, Kp, step, ok);
-                asm volatile("" : "+v"(ok));
-                o[q].z = pll_step_fast(p, ctx, src[q].z, Ki, Kp, step, ok);
-                asm volatile("" : "+v"(ok));
-                o[q].w = pll_step_fast(p, ctx, src[q].w, Ki, Kp, step, ok);
-                asm volatile("" : "+v"(ok));
-            }
-            if (!ok) {  // rare: redo from the saved state on the exact path
+                for (int q = 0; q < kPllBatch / 4; q++)
+                    reinterpret_cast<float4*>(x + b * kPllBatch)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
+            } else {  // rare: redo from the saved state on the exact path
                 p = p0;
                 ctx = ctx0;
                 float* xb = x + b * kPllBatch;
 #pragma unroll 1
                 for (int j = 0; j < kPllBatch; j++) xb[j] = pll_step(p, ctx, xb[j], Ki, Kp, step, lib);
-            } else {
-#pragma unroll
-                for (int q = 0; q < 4; q++) reinterpret_cast<float4*>(x + b * kPllBatch)[q] = o[q];
             }
         };
         if (nb > 0) load(A, 0);

@@ -5,6 +5,9 @@
 // Modes:
 //   sincos <lo> <hi> <stride>   every `stride`-th float in [lo, hi] (both signs)
 //   atan2  <n> <seed>           n random float pairs from several distributions
+//   rot    <n> <seed>           the PLL's rotation atan2 (rot_atan2_f): n random (trigArg x,
+//                               sample v) pairs, context from sincos_ctx_f(x), fb = glibc's
+//                               float cos/sin of x, checked against glibc atan2(eQ, eI)
 // Prints counts: checked, fast-path hits, fallbacks, MISMATCHES (must be 0).
 #include <cmath>
 #include <cstdint>
@@ -67,6 +70,48 @@ int main(int argc, char** argv) {
                         } else {
                             c.fb2++;
                         }
+                    }
+                }
+            });
+    } else if (!std::strcmp(argv[1], "rot")) {
+        const unsigned long long n = std::atoll(argv[2]);
+        const uint64_t seed = std::atoll(argv[3]);
+        for (int t = 0; t < T; t++)
+            th.emplace_back([&, t] {
+                Count& c = cnt[t];
+                for (unsigned long long i = t; i < n; i += T) {
+                    const uint64_t h = sm64(seed * 0x7654321ull + i), h2 = sm64(h);
+                    float x;
+                    switch (h % 4) {
+                        case 0: x = (float)((int32_t)h) * 4.0e-3f; break;                      // |x| < 8.6e6
+                        case 1: x = (float)((int32_t)h) * 1.0e-9f; break;                      // |x| < 2.2
+                        case 2: x = (float)((double)((int32_t)(h >> 8) >> 8) * 1.5707963267948966 +
+                                             (double)((int32_t)h2) * 1e-14); break;            // near k pi/2
+                        default: x = bits2f((uint32_t)(h >> 32) & 0x4EFFFFFFu) * ((h & 8) ? -1.0f : 1.0f); break;
+                    }
+                    float v;
+                    switch (h2 % 3) {
+                        case 0: v = (float)((int32_t)(h2 >> 16)) * 2.3e-11f; break;
+                        case 1: v = (float)((int32_t)(h2 >> 16)) * 1.7e-3f; break;
+                        default: v = bits2f((uint32_t)(h2 >> 32)); break;                     // any bits
+                    }
+                    if (std::isnan(v) || std::isinf(v)) continue;
+                    fmrx::PllCtx ctx{};
+                    float s2, c2;
+                    fmrx::sincos_ctx_f(x, &s2, &c2, &ctx);
+                    const float fbI = (float)std::cos((double)x), fbQ = (float)std::sin((double)x);
+                    const float eI = v * fbI, eQ = v * (-fbQ);
+                    float a;
+                    c.n++;
+                    if (fmrx::rot_atan2_f(eQ, eI, ctx, &a)) {
+                        c.fast++;
+                        const float g = (float)std::atan2((double)eQ, (double)eI);
+                        if (f2bits(a) != f2bits(g)) {
+                            if (c.bad < 5) std::printf("MISMATCH rot x=%.9g v=%.9g fast=%.9g glibc=%.9g\n", x, v, a, g);
+                            c.bad++;
+                        }
+                    } else {
+                        c.fb++;
                     }
                 }
             });

@@ -1,7 +1,8 @@
 // tools/check_pll_run.cpp — run the whole PLL recurrence (src/filter.cpp:136-174) two ways on
 // the host and require bit-identical output: (a) the reference's arithmetic with glibc's
 // double atan2/cos/sin, (b) csrc/pll_math.h's pll_step (certified fast paths + glibc
-// fallbacks), i.e. exactly what pll_kernel executes on the GPU.
+// fallbacks), (c) pll_kernel's schedule: 16-sample pll_batch_fast batches, a batch redone with
+// pll_step when it cannot be certified, the tail with pll_step -- the GPU's arithmetic.
 // Usage: check_pll_run <carrier.f32> <freq> <fs> [chunk]   (state carried across chunks)
 #include <cmath>
 #include <algorithm>
@@ -66,7 +67,42 @@ int main(int argc, char** argv) {
             }
         }
     }
-    const bool state_ok = p.integ == integ && p.phase == phase && p.fbI == fbI && p.fbQ == fbQ && p.trig == trig;
-    std::printf("samples=%zu mismatches=%zu state_equal=%d\n", x.size(), bad, (int)state_ok);
-    return (bad || !state_ok) ? 1 : 0;
+    bool state_ok = p.integ == integ && p.phase == phase && p.fbI == fbI && p.fbQ == fbQ && p.trig == trig;
+    // (c) batches as in pll_kernel
+    constexpr int NB = 16;
+    fmrx::PllState pb{0, 0, 1, 0, 0};
+    size_t bad_c = 0, batches = 0, redone = 0;
+    for (size_t c0 = 0; c0 < x.size(); c0 += chunk) {
+        fmrx::PllCtx ctx{};
+        ctx.valid = false;
+        const size_t c1 = std::min(x.size(), c0 + chunk);
+        std::vector<float> out(c1 - c0);
+        size_t i = c0;
+        for (; i + NB <= c1; i += NB) {
+            float v[NB], o[NB];
+            std::memcpy(v, &x[i], sizeof v);
+            const fmrx::PllState p0 = pb;
+            const fmrx::PllCtx ctx0 = ctx;
+            batches++;
+            if (!fmrx::pll_batch_fast(pb, ctx, v, o, Ki, Kp, step)) {
+                redone++;
+                pb = p0;
+                ctx = ctx0;
+                for (int j = 0; j < NB; j++) o[j] = fmrx::pll_step(pb, ctx, v[j], Ki, Kp, step, lib);
+            }
+            std::memcpy(&out[i - c0], o, sizeof o);
+        }
+        for (; i < c1; i++) out[i - c0] = fmrx::pll_step(pb, ctx, x[i], Ki, Kp, step, lib);
+        for (size_t k = c0; k < c1; k++) {
+            const float nco = (float)std::cos((double)(out[k - c0] * 2.0f + 0.0f));
+            if (std::memcmp(&nco, &ref[k], 4) != 0) {
+                if (bad_c < 5) std::printf("MISMATCH (batch) at %zu: %.9g vs %.9g\n", k, nco, ref[k]);
+                bad_c++;
+            }
+        }
+    }
+    state_ok = state_ok && pb.integ == integ && pb.phase == phase && pb.fbI == fbI && pb.fbQ == fbQ && pb.trig == trig;
+    std::printf("batches=%zu redone=%zu\n", batches, redone);
+    std::printf("samples=%zu mismatches=%zu state_equal=%d\n", x.size(), bad + bad_c, (int)state_ok);
+    return (bad || bad_c || !state_ok) ? 1 : 0;
 }
