@@ -1,0 +1,17 @@
+#!/bin/bash
+# One GPU session for the stereo/RDS engine: full GPU test suite, RDS and stereo benches,
+# config-5 per-GPU share through the distributed runner, and a kernel-trace profile of the
+# single-stream stereo bench.  Usage (on the GPU box via gpurun): bash tools/gpu_stereo_round.sh <tag>
+set -o pipefail
+TAG=${1:-stereo}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1 || exit 1
+timeout -k 10 300 python tools/bench_stereo.py --streams 1 32 256 > $OUT/bench_stereo.json 2> $OUT/bench_stereo.err || exit 2
+timeout -k 10 300 python tools/bench_rds.py --streams 1,256 > $OUT/bench_rds.json 2> $OUT/bench_rds.err || exit 3
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+    --master-port 29531 tools/bench_streams.py --streams 32 --seconds 10 --check > $OUT/bench_streams32.json 2> $OUT/bench_streams32.err || exit 4
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/kt_stereo -o run --output-format csv -- \
+    python3 tools/bench_stereo.py --streams 1 > $OUT/kt_stereo.log 2>&1 || exit 5
+echo done
