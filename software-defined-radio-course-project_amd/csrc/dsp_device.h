@@ -17,11 +17,14 @@ __host__ __device__ inline float u8_to_sample(uint32_t u) {
 
 // src/filter.cpp:110-127, one sample of FMDemod.  The denominator is std::pow(float, 2)
 // summed in double then rounded to float; the quotient is an IEEE float division.
+// A float squared is exact in double (48 significant bits), so the reference's rounded sum
+// of the two squares is one fma of the second square onto the first: the same single
+// rounding, one instruction fewer.
 __host__ __device__ inline float fm_demod_one(float ci, float cq, float pi, float pq) {
     const float di = ci - pi;
     const float dq = cq - pq;
-    const float den = static_cast<float>(static_cast<double>(ci) * static_cast<double>(ci) +
-                                         static_cast<double>(cq) * static_cast<double>(cq));
+    const double cid = static_cast<double>(ci), cqd = static_cast<double>(cq);
+    const float den = static_cast<float>(__builtin_fma(cqd, cqd, cid * cid));
     // The quotient is formed unconditionally and selected (no divergent branch on device);
     // den == 0 gives 0 exactly as filter.cpp:125-129.
     const float num = (ci * dq) - (cq * di);

@@ -59,6 +59,17 @@ struct MonoCfg {
     static constexpr int NLD = (P / 2 + NT - 1) / NT;   // 4-B (2-pair) loads per thread/chunk
     static constexpr int CAmax = (CIF + AD - 1) / AD;   // max audio outputs in one chunk
     static constexpr int NG = (T + 1) / 2;              // tap groups: {0}, {1,2}, {3,4}, ...
+    // Audio window (modes 0/1): GA consecutive chunks of demod are gathered before the audio
+    // FIR runs once over them, two outputs per lane in packed ops: lane t owns window outputs
+    // t and t + NA, whose samples are DX = AD NA apart.  The window (50 history samples + GA
+    // chunks) is stored as DX + 50 float2 (sample s, sample s + DX), so one ds_read_b64 gives
+    // a tap's two samples.  GA is the largest count (<= 3) whose outputs fit two per lane.
+    static constexpr int na_for(int g) { return ((g * CIF + AD - 1) / AD + 1) / 2; }
+    static constexpr int GA = na_for(3) <= NT ? 3 : na_for(2) <= NT ? 2 : 1;
+    static constexpr int NA = na_for(GA);
+    static constexpr int DX = AD * NA;
+    static constexpr int DWI = DX + 50;  // float2 entries: sample s in .x (s < DX + 50), in .y (s >= DX)
+    static_assert(2 * DX >= GA * CIF, "every window sample has a slot");
     static_assert(T % 2 == 1, "odd tap count");
     static_assert(S % 2 == 0 && H % 2 == 0, "pair groups must stay 16-B aligned");
     static_assert(P % 2 == 0, "chunk must be whole dwords");
@@ -114,12 +125,22 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     constexpr bool kShfl = NT == 64;
     static_assert(AU == 1 || ((long long)CIF * AU + AD - 1) / AD + 1 <= NT, "one audio output per thread");
 
+    constexpr bool kWin = AU == 1;               // windowed packed audio stage (modes 0/1)
+    constexpr int GA = C::GA;
     __shared__ float4 xb4[C::XB / 2 + 1];        // scaled (I,Q) pairs, two per float4
-    __shared__ float dbuf[2][kAH + CIF];         // demod window: 50 history + chunk
+    // demod: modes 0/1 the paired audio window (50 history + GA chunks); modes 2/3 two
+    // alternating 50 + chunk windows
+    __shared__ float2 dwi[kWin ? C::DWI : 1];
+    __shared__ float dbuf[kWin ? 1 : 2][kWin ? 1 : kAH + CIF];
     __shared__ float2v pbuf[kShfl ? 1 : 2][kShfl ? 1 : NT + 1];  // last RF output per thread
-    __shared__ float2 ctab2[NG + 1];             // (c[2j-1], c[2j]); c[-1] = 0
+    __shared__ float2 ctab2[TR ? 1 : NG + 1];    // (c[2j-1], c[2j]); c[-1] = 0 (TR = 0 only)
     __shared__ float atab[kAudioTaps + 1];       // audio taps
     float* ctab = reinterpret_cast<float*>(ctab2);
+    // window sample s (0..49 history, 50.. the GA chunks)
+    auto wput = [&](int s, float v) {
+        if (s < C::DWI) dwi[s].x = v;
+        if (s >= C::DX) dwi[s - C::DX].y = v;
+    };
 
     const int tid = threadIdx.x;
     const int stream = blockIdx.x / L.segs;
@@ -140,7 +161,8 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     const long long total = (long long)L.stream_bytes;
     const long long hb = (long long)L.halo_bytes;
 
-    for (int i = tid; i < 2 * (NG + 1); i += NT) ctab[i] = (i >= 1 && i <= T) ? taps.rf[i - 1] : 0.0f;
+    if constexpr (TR == 0)
+        for (int i = tid; i < 2 * (NG + 1); i += NT) ctab[i] = (i >= 1 && i <= T) ? taps.rf[i - 1] : 0.0f;
     for (int i = tid; i < kAudioTaps; i += NT) atab[i] = taps.audio[i];
 
     // ---- prologue: RF history in front of the pre-roll chunk (pairs [(c0-1)P - H, (c0-1)P))
@@ -170,10 +192,9 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     fetch(c0 - 1);
 
     float2 creg[TR ? NG : 1];
-    if constexpr (TR != 0) {
-        __syncthreads();
+    if constexpr (TR != 0) {  // straight from the kernel arguments (scalar loads)
 #pragma unroll
-        for (int j = 0; j < NG; j++) creg[j] = ctab2[j];
+        for (int j = 0; j < NG; j++) creg[j] = make_float2(j == 0 ? 0.0f : taps.rf[2 * j - 1], taps.rf[2 * j]);
     }
     int cur = 0;
     // (c0-1) CIF = AD aq + ar; for c0 = 0 this is (-(CIF/AD), -(CIF%AD)), which the first
@@ -181,6 +202,9 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     long long aq = (long long)(c0 - 1) * CIF / AD;
     int ar = (int)((long long)(c0 - 1) * CIF - aq * AD);
     float2v carry = {0.0f, 0.0f};  // NT = 64: last RF output of the previous chunk
+    int slot = -1;                 // audio window slot of chunk c (-1: the pre-roll chunk)
+    long long wm0 = 0;             // first audio output of the current window
+    int woff0 = 0;                 // its IF offset from the window start
     for (int c = c0 - 1; c < c1; c++) {
         // ---- stage chunk c: lane u writes pairs H+2u, H+2u+1 as one float4; consecutive
         // lanes write consecutive 16-B slots (conflict-free ds_write_b128).
@@ -271,11 +295,11 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         }
         // Pin the accumulators here: without it LLVM sinks the pure-register FIR chains past
         // the barrier to their first use (demod), keeping the whole sample window live.
+        // The accumulators stay scaled by 2^7: FMDemod is invariant under an exact power-of-2
+        // scaling of every I/Q (num and den scale by 2^14, every rounding with them; all
+        // values are far from the subnormal and overflow ranges), and nothing else reads them.
 #pragma unroll
-        for (int r = 0; r < R; r++) {
-            asm volatile("" ::"v"(acc[r]));
-            acc[r] = acc[r] * 0.0078125f;  // undo the 2^7 sample scaling (exact)
-        }
+        for (int r = 0; r < R; r++) asm volatile("" ::"v"(acc[r]));
         if constexpr (!kShfl) pbuf[cur][tid + 1] = acc[R - 1];
         __syncthreads();  // (B) all RF reads of xb done, pbuf visible
 
@@ -303,11 +327,26 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                 d[r] = fm_demod_one(acc[r].x, acc[r].y, pv.x, pv.y);
         }
         const long long g0 = (long long)c * CIF + R * tid;  // IF index of d[0]
+        if constexpr (kWin) {
+            // window slot `slot` of the audio window; the pre-roll chunk (slot -1) leaves only
+            // its last 50 samples, as the first window's history
+            if (L.audio) {
 #pragma unroll
-        for (int r = 0; r < R; r++) {
-            const int jl = R * tid + r;
-            dbuf[cur][kAH + jl] = d[r];
-            if (jl >= CIF - kAH) dbuf[cur ^ 1][jl - (CIF - kAH)] = d[r];
+                for (int r = 0; r < R; r++) {
+                    const int jl = R * tid + r;
+                    if (slot >= 0)
+                        wput(kAH + slot * CIF + jl, d[r]);
+                    else if (jl >= CIF - kAH)
+                        wput(jl - (CIF - kAH), d[r]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int jl = R * tid + r;
+                dbuf[cur][kAH + jl] = d[r];
+                if (jl >= CIF - kAH) dbuf[cur ^ 1][jl - (CIF - kAH)] = d[r];
+            }
         }
         // Demod to global only for the split API / the chunk holding the stream's last 50
         // samples (one scalar test per chunk; the fused mono path skips it otherwise).
@@ -324,6 +363,10 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
             }
         }
         __syncthreads();  // (C) demod window complete
+        // (c+1) CIF = AD aq1 + ar1
+        long long aq1 = aq + CIF / AD;
+        int ar1 = ar + CIF % AD;
+        if (ar1 >= AD) { ar1 -= AD; aq1++; }
 
         // ---- audio LPF + decimate + quantise: outputs m with AD*m in this chunk.  Chunk c
         // starts at IF index pos = c CIF = AD aq + ar (tracked incrementally); its first audio
@@ -354,28 +397,52 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                     if (L.mono) L.mono[oi] = a;
                 }
             }
-        } else if (L.audio && c >= c0) {
-            const int off0 = ar > 0 ? AD - ar : 0;
-            const long long m0 = aq + (ar > 0);
-            const long long left = n_audio - m0;  // outputs of the stream not yet written
-            if (tid < C::CAmax && off0 + AD * tid < CIF && tid < left) {
-                const long long m = m0 + tid;
-                const float* dw = &dbuf[cur][off0 + AD * tid + kAH];
-                float a = 0.0f;
+        } else if (L.audio && slot >= 0) {
+            // mono audio LPF + decimate (project.cpp:146, up = 1) over the window of chunks
+            // c - slot .. c, run once the window is full (or the segment ends).  Lane t owns
+            // window outputs t and t + NA and advances them together in packed ops: each is
+            // still an ascending-tap sequential sum of separately rounded products
+            // (filter.cpp:84-92).
+            if (slot == 0) {  // first output of the window and its offset in the window
+                wm0 = aq + (ar > 0);
+                woff0 = ar > 0 ? AD - ar : 0;
+            }
+            if (slot == GA - 1 || c == c1 - 1) {
+                long long mend = aq1 + (ar1 > 0);  // first output of the next window
+                if (mend > n_audio) mend = n_audio;
+                const long long nw = mend - wm0;
+                if (tid < C::NA && tid < nw) {
+                    // base[kAH - k] = (sample o_a - k, sample o_a + DX - k), o_a = woff0 + AD t
+                    const float2* base = dwi + woff0 + AD * tid;
+                    float2v a2 = {0.0f, 0.0f};
 #pragma unroll
-                for (int k = 0; k < ((ABL & 2) != 0 ? 1 : kAudioTaps); k++) {
-                    const float p = atab[k] * dw[-k];
-                    a = a + p;
+                    for (int k = 0; k < ((ABL & 2) != 0 ? 1 : kAudioTaps); k++) {
+                        const float2 xs = base[kAH - k];
+                        const float2v p = float2v{xs.x, xs.y} * atab[k];
+                        a2 = a2 + p;
+                    }
+                    const size_t oi = (size_t)stream * (size_t)n_audio + (size_t)(wm0 + tid);
+                    L.pcm[oi] = quantize_s16(a2.x);
+                    if (L.mono) L.mono[oi] = a2.x;
+                    if (tid + C::NA < nw) {
+                        L.pcm[oi + C::NA] = quantize_s16(a2.y);
+                        if (L.mono) L.mono[oi + C::NA] = a2.y;
+                    }
                 }
-                const size_t oi = (size_t)stream * (size_t)n_audio + (size_t)m;
-                L.pcm[oi] = quantize_s16(a);
-                if (L.mono) L.mono[oi] = a;
+                if (slot == GA - 1) {
+                    __syncthreads();  // window reads done: its last 50 samples become history
+                    // sample GA CIF + i (>= DX) sits in .y of entry GA CIF + i - DX
+                    float h = 0.0f;
+                    if (tid < kAH) h = dwi[GA * CIF + tid - C::DX].y;
+                    __syncthreads();
+                    if (tid < kAH) wput(tid, h);
+                }
             }
         }
         cur ^= 1;
-        aq += CIF / AD;
-        ar += CIF % AD;
-        if (ar >= AD) { ar -= AD; aq++; }
+        aq = aq1;
+        ar = ar1;
+        if constexpr (kWin) slot = slot + 1 == GA ? 0 : slot + 1;
     }
 }
 
