@@ -55,7 +55,7 @@ typedef struct {
     int channels;    /* FMRX_MONO or FMRX_STEREO                                              */
     int rf_taps;     /* RF LPF taps, reference 51 (project.cpp:306); 0 = default              */
     int bp_taps;     /* stereo band-pass taps, reference 51 (project.cpp:307); 0 = default   */
-    int audio_taps;  /* audio LPF taps per phase, reference 51 (project.cpp:319; x up in 2/3) */
+    int audio_taps;  /* audio LPF taps per phase: 51 only (project.cpp:319; x up in 2/3)    */
     int n_streams;   /* independent IQ streams processed per call (>=1)                        */
     int device;      /* HIP device ordinal                                                     */
 } fmrx_config;

@@ -81,6 +81,7 @@ struct fmrx_ctx {
     std::vector<float> rf, audio, ch, ca;
     MonoTaps mono_taps{};
     DevBuf<float> d_audio, d_rf;
+    DevBuf<float> d_audio_rows;   // modes 2/3: the audio prototype by phase (kAudioRow floats per row)
     // RF state: the raw bytes preceding the next call, double-buffered
     size_t halo_bytes = 0;
     DevBuf<uint8_t> d_halo[2];
@@ -253,6 +254,7 @@ int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
     L.demod_tail = with_audio ? c->d_audio_hist.p + (c->audio_hist - kAudioHist50) : nullptr;
     L.demod_tail_stride = (size_t)c->audio_hist;
     L.audio_coeff = c->d_audio.p;
+    L.audio_rows = c->d_audio_rows.p;
     L.stream_bytes = n_blocks * c->geo.block_bytes;
     L.halo_bytes = c->halo_bytes;
     L.n_if = (long long)(n_blocks * c->geo.if_samples);
@@ -406,8 +408,9 @@ int fmrx_geometry(const fmrx_config* cfg, fmrx_geometry_t* g) {
     const int audio_taps = cfg->audio_taps ? cfg->audio_taps : 51;
     if (rf_taps < 3 || rf_taps > kMaxRfTaps) return fail(FMRX_EINVAL, "rf_taps %d out of range", rf_taps);
     if (bp_taps < 3 || bp_taps > 64) return fail(FMRX_EINVAL, "bp_taps %d out of range", bp_taps);
-    if (audio_taps < 3 || audio_taps > kMaxAudioTaps)
-        return fail(FMRX_EINVAL, "audio_taps %d out of range", audio_taps);
+    // The fused audio stages (mono window, rational resampler rows, stereo LPFs' shared
+    // 50-sample history) are compiled for the reference's 51 taps per phase (project.cpp:319).
+    if (audio_taps != 51) return fail(FMRX_EINVAL, "audio_taps %d unsupported (51 per phase)", audio_taps);
     g->rf_fs = m.rf_fs;
     g->rf_decim = m.rf_decim;
     g->if_fs = m.if_fs;
@@ -487,6 +490,17 @@ int fmrx_create(const fmrx_config* cfg, fmrx_ctx** out) {
         hipMemcpy(c->d_rf.p, c->rf.data(), sizeof(float) * c->rf.size(), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->d_sintab.p, synth_sintab(), sizeof(int16_t) * kSinSize, hipMemcpyHostToDevice) != hipSuccess)
         return cleanup(fail(FMRX_EHIP, "tap upload failed"));
+    if (g.audio_up > 1) {
+        // the rational resampler's prototype by phase: row k0 holds the 51 taps an output of
+        // phase k0 reads, in the order filter.cpp:84 visits them (k = k0, k0 + up, ...)
+        const int up = g.audio_up;
+        std::vector<float> rows((size_t)up * kAudioRow, 0.0f);
+        for (int k0 = 0; k0 < up; k0++)
+            for (int i = 0; i < 51; i++) rows[(size_t)k0 * kAudioRow + i] = c->audio[(size_t)k0 + (size_t)i * up];
+        if ((rc = c->d_audio_rows.ensure(rows.size()))) return cleanup(rc);
+        if (hipMemcpy(c->d_audio_rows.p, rows.data(), sizeof(float) * rows.size(), hipMemcpyHostToDevice) != hipSuccess)
+            return cleanup(fail(FMRX_EHIP, "tap upload failed"));
+    }
     if ((rc = reset_state(c))) return cleanup(rc);
     *out = c;
     return FMRX_OK;
@@ -496,7 +510,7 @@ void fmrx_destroy(fmrx_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->cfg.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    c->d_audio.release(); c->d_rf.release(); c->d_halo[0].release(); c->d_halo[1].release();
+    c->d_audio.release(); c->d_rf.release(); c->d_audio_rows.release(); c->d_halo[0].release(); c->d_halo[1].release();
     c->d_audio_hist.release(); c->d_demod.release(); c->d_channel.release(); c->d_carrier.release();
     c->d_pll.release(); c->d_mix_tail.release(); c->d_mono_state.release(); c->d_in.release();
     c->d_out.release(); c->d_f32.release(); c->d_scratch.release(); c->d_sintab.release();

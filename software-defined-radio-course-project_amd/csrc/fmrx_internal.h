@@ -23,6 +23,7 @@ constexpr int kRfFc = 100000;   // src/project.cpp:304
 constexpr int kAudioFc = 16000; // src/project.cpp:305
 
 constexpr int kMaxAudioTaps = 64;
+constexpr int kAudioRow = 52;   // one polyphase phase of the 51-taps-per-phase audio prototype, 16-B rows
 
 // Coefficient tables handed to kernels by value (kernarg segment -> scalar registers).
 struct MonoTaps {
@@ -44,6 +45,8 @@ struct MonoLaunch {
                                 //   s * demod_tail_stride for stream s
     size_t demod_tail_stride;
     const float* audio_coeff;   // modes 2/3: the rational resampler's prototype (device)
+    const float* audio_rows;    // modes 2/3: the same taps as `up` rows of kAudioRow floats,
+                                //   row k0 = coeff[k0 + i up] for i < 51 (then zeros)
     size_t stream_bytes;        // n_blocks * block_bytes
     size_t halo_bytes;
     long long n_if;             // IF samples per stream this call

@@ -203,6 +203,9 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     int ar = (int)((long long)(c0 - 1) * CIF - aq * AD);
     float2v carry = {0.0f, 0.0f};  // NT = 64: last RF output of the previous chunk
     int slot = -1;                 // audio window slot of chunk c (-1: the pre-roll chunk)
+    // modes 2/3: lane t's resampler offset t AD = au_qt AU + au_rt
+    const int au_qt = AU > 1 ? tid * AD / AU : 0;
+    const int au_rt = AU > 1 ? tid * AD - au_qt * AU : 0;
     long long wm0 = 0;             // first audio output of the current window
     int woff0 = 0;                 // its IF offset from the window start
     for (int c = c0 - 1; c < c1; c++) {
@@ -376,21 +379,36 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
             // k0 = (m AD) mod AU and base j0 = floor(m AD / AU); it reads demod j0 - i, i < 51,
             // against coeff[k0 + i AU] (i ascending = k ascending, filter.cpp:84-92), and
             // belongs to the chunk that holds j0 (its 50 predecessors are the window history)
+            // Lane t takes output mlo + t: with t AD = qt AU + rt (per lane, once) and
+            // mlo AD = qb AU + rb (per chunk, scalar), j0 and k0 follow without a division.
+            // The output's 51 taps are row k0 of L.audio_rows, read as 16-B vectors.
             if (L.audio && c >= c0) {
                 const long long mlo = ((long long)c * CIF * AU + AD - 1) / AD;
                 const long long mhi = ((long long)(c + 1) * CIF * AU + AD - 1) / AD;
                 const long long m = mlo + tid;
                 if (m < mhi && m < n_audio) {
-                    const long long nd = m * AD;
-                    const long long j0 = nd / AU;
-                    const int k0 = (int)(nd - j0 * AU);
-                    const float* dw = &dbuf[cur][kAH + (int)(j0 - (long long)c * CIF)];
-                    const float* cf = L.audio_coeff + k0;
+                    const long long nb = mlo * AD;
+                    const long long qb = nb / AU;
+                    const int rb = (int)(nb - qb * AU);
+                    const int rr = rb + au_rt;
+                    const int wrap = rr >= AU ? 1 : 0;
+                    const int k0 = rr - wrap * AU;
+                    const int jl = (int)(qb - (long long)c * CIF) + au_qt + wrap;  // j0 - c CIF
+                    const float* dw = &dbuf[cur][kAH + jl];
+                    const float4* row = reinterpret_cast<const float4*>(L.audio_rows + (size_t)k0 * kAudioRow);
                     float a = 0.0f;
 #pragma unroll
-                    for (int i = 0; i < kAudioTaps; i++) {
-                        const float p = cf[i * AU] * dw[-i];
-                        a = a + p;
+                    for (int i4 = 0; i4 < kAudioRow / 4; i4++) {
+                        const float4 cq = row[i4];
+                        const float cv[4] = {cq.x, cq.y, cq.z, cq.w};
+#pragma unroll
+                        for (int e = 0; e < 4; e++) {
+                            const int i = 4 * i4 + e;
+                            if (i < kAudioTaps) {
+                                const float p = cv[e] * dw[-i];
+                                a = a + p;
+                            }
+                        }
                     }
                     const size_t oi = (size_t)stream * (size_t)n_audio + (size_t)m;
                     L.pcm[oi] = quantize_s16(a);

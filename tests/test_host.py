@@ -54,7 +54,8 @@ def test_geometry_matches_survey_table_m(fmrx, mode, channels):
 
 
 @pytest.mark.parametrize("bad", [dict(mode=4), dict(mode=-1), dict(channels=3), dict(channels=0),
-                                 dict(rf_taps=1), dict(rf_taps=1000), dict(bp_taps=200)])
+                                 dict(rf_taps=1), dict(rf_taps=1000), dict(bp_taps=200),
+                                 dict(audio_taps=31), dict(audio_taps=64)])
 def test_invalid_config_rejected(fmrx, bad):
     cfg = fmrx.Config(0, 1, 51, 51, 51, 1, 0)
     for k, v in bad.items():
