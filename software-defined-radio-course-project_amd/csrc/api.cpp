@@ -108,6 +108,7 @@ struct fmrx_ctx {
     DevBuf<int16_t> d_out;
     DevBuf<float> d_f32;
     DevBuf<float> d_scratch;
+    DevBuf<double> d_pll_side;    // PLL side data of one segment (pll_side_doubles)
     DevBuf<int16_t> d_sintab;
     // kernel timing: pairs of HIP events recorded around each fused-kernel launch on the
     // context stream (no host sync inside the timed loop); read by fmrx_kernel_timing
@@ -197,6 +198,7 @@ int run_rds(fmrx_ctx* c, const float* d_demod, size_t demod_stride, size_t n_if,
         c->rds_chan_stride = stride;
     }
     int rc = c->d_rds_car.ensure(n_if * ns);
+    if (!rc) rc = c->d_pll_side.ensure(pll_side_doubles((int)n_if, ns));
     if (rc) return rc;
     RdsLaunch L{};
     L.demod = d_demod;
@@ -209,6 +211,7 @@ int run_rds(fmrx_ctx* c, const float* d_demod, size_t demod_stride, size_t n_if,
     L.out = d_out;
     L.out_stride = n_if;
     L.pll = c->d_rds_pll.p;
+    L.pll_side = c->d_pll_side.p;
     L.ex = c->d_rds_taps.p;
     L.ca = c->d_rds_taps.p + kRdsTaps;
     L.bp_fs = (float)c->geo.bp_fs;
@@ -324,8 +327,9 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
     S.bp_taps = c->geo.bp_taps;
     if (launch_bpf_pair(S, ns, c->stream)) return fail(FMRX_EHIP, "band-pass launch failed");
     // project.cpp:166: PLL(carrier, 19000, if_fs, 2, 0, 0.01, ...)
+    if ((rc = c->d_pll_side.ensure(pll_side_doubles((int)n_if, ns)))) return rc;
     if (launch_pll(c->d_carrier.p, (int)n_if, ns, n_if, 19000.0f, (float)c->geo.if_fs, 2.0f, 0.0f,
-                   0.01f, c->d_pll.p, c->stream))
+                   0.01f, c->d_pll.p, c->d_pll_side.p, c->stream))
         return fail(FMRX_EHIP, "PLL launch failed");
     AudioLaunch A{};
     A.demod = c->d_demod.p;
@@ -514,6 +518,7 @@ void fmrx_destroy(fmrx_ctx* c) {
     c->d_audio_hist.release(); c->d_demod.release(); c->d_channel.release(); c->d_carrier.release();
     c->d_pll.release(); c->d_mix_tail.release(); c->d_mono_state.release(); c->d_in.release();
     c->d_out.release(); c->d_f32.release(); c->d_scratch.release(); c->d_sintab.release();
+    c->d_pll_side.release();
     c->d_rds_taps.release(); c->d_rds_dhist.release(); c->d_rds_chan.release(); c->d_rds_car.release();
     c->d_rds_pll.release();
     for (auto& e : c->evs) {
@@ -854,7 +859,9 @@ int fmrx_pll(fmrx_ctx* c, float* d_io, int n, float freq, float fs, float nco_sc
     rc = c->d_scratch.ensure(8);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(c->d_scratch.p, d_st, 6 * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
-    if (launch_pll(d_io, n, 1, (size_t)n, freq, fs, nco_scale, phase_adjust, norm_bw, c->d_scratch.p, c->stream))
+    if ((rc = c->d_pll_side.ensure(pll_side_doubles(n, 1)))) return rc;
+    if (launch_pll(d_io, n, 1, (size_t)n, freq, fs, nco_scale, phase_adjust, norm_bw, c->d_scratch.p,
+                   c->d_pll_side.p, c->stream))
         return fail(FMRX_EHIP, "launch failed");
     HIPCHK(hipMemcpyAsync(d_st, c->d_scratch.p, 6 * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
     return FMRX_OK;

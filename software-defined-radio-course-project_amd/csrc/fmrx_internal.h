@@ -80,8 +80,12 @@ struct StereoLaunch {
     int bp_taps;
 };
 int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s);
+// PLL over n samples of n_streams streams (state st, 8 floats per stream), then the NCO
+// (filter.cpp:136-174).  side: device scratch of pll_side_doubles(n, n_streams) doubles.
+constexpr size_t kPllSeg = (size_t)1 << 18;  // samples per stream per PLL launch
+size_t pll_side_doubles(int n, int n_streams);
 int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
-               float nco_scale, float phase_adjust, float norm_bw, float* st, hipStream_t s);
+               float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s);
 
 struct AudioLaunch {
     const float* demod;     // with hist samples in front (per stream stride demod_stride)
@@ -115,6 +119,7 @@ struct RdsLaunch {
     float* out;             // n_streams x n_if: mixer output
     size_t out_stride;
     float* pll;             // n_streams x 8 PLL state
+    double* pll_side;       // pll_side_doubles(n_if, n_streams) scratch
     const float* ex;        // 54-60 kHz taps (device)
     const float* ca;        // 113.5-114.5 kHz taps (device)
     float bp_fs;

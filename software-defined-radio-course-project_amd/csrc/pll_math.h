@@ -278,60 +278,126 @@ FMRX_HD float pll_step(PllState& p, PllCtx& ctx, float v, float Ki, float Kp, do
     return arg;
 }
 
+// ---- per-sample side data of a segment (pll_prep_kernel, parallel over samples) -----------
+//
+// Everything of a step that depends only on the input and the step index is computed ahead,
+// in parallel, so the serial loop keeps only the recurrence:
+//   iv_j = 1 / v_j in double -- the quotient Y / X of the rotation atan2 without a reciprocal
+//          (below); NaN when |v_j| < kPllMinV or v_j is not finite, so the batch fails its
+//          NaN check and is redone exactly;
+//   pr_j = step * (double)trig_j, trig_j = the float trigOffset after step j's increment
+//          (filter.cpp:165-166).  From an integer-valued t0 in [0, 2^24] the float increments
+//          are exact up to 2^24 and then stick there, so trig_j = min(t0 + j + 1, 2^24); any
+//          other t0 (reachable only through fmrx_set_state) or |pr_j| >= kPllMaxPr gives NaN.
+constexpr double kPllMaxPr = 4.0e8;
+constexpr float kPllMaxPhase = 5.0e8f;  // with |pr| < 4e8: |trigArg| < kPllMaxX over a batch
+constexpr float kPllMaxInteg = 1.0e6f;
+constexpr float kPllTrigStick = 16777216.0f;  // 2^24: trigOffset + 1.0f == trigOffset from here
+
+FMRX_HD bool pll_trig_domain(float t0) {
+    return t0 >= 0.0f && t0 <= kPllTrigStick && t0 == floorf(t0);
+}
+
+FMRX_HD void pll_side(float v, float t0, long long j, double step, double* iv, double* pr) {
+    const double vd = (double)v;
+    *iv = (fabs(vd) >= (double)kPllMinV && fabs(vd) < 1.0e300) ? 1.0 / vd : (double)NAN;
+    const float trig = (float)fmin((double)t0 + (double)(j + 1), (double)kPllTrigStick);
+    const double p = step * (double)trig;
+    *pr = (pll_trig_domain(t0) && fabs(p) < kPllMaxPr) ? p : (double)NAN;
+}
+
+// pll_offset with the half-integer m - hneg times 2 pi: (m - hneg) 2pi_hi is the same exact
+// product as J pi_hi inside the fma, so B is bit-identical, one operation shorter.
+constexpr double k2PiHi = 2.0 * kPiHi, k2PiLo = 2.0 * kPiLo;
+FMRX_HD double pll_offset_h(double x, double hneg) {
+    const double mh = rint(fma(x, kInv2Pi, hneg)) - hneg;
+    return fma(mh, k2PiLo, fma(mh, k2PiHi, -x));
+}
+
+// decide_float_16ulp's margin scaled by 8: (low dword << 3) - (2^31 - 128), one shift-add;
+// > 256 iff the float rounding of v is certified.
+FMRX_HD uint32_t pll_margin16x8(double v) {
+    return ((uint32_t)__builtin_bit_cast(uint64_t, v) << 3) + 0x80000080u;
+}
+
 // N steps straight-line on the certified fast paths, with no branch and no quadrant work
 // (the representation above): the loop carries (fc, nfs, cs, sn, B) and folds every
 // certification into a few accumulators checked once at the end.  Returns true when every
 // step was certified -- the outputs and (p, ctx) then equal N pll_step calls bit for bit.
 // Otherwise p and ctx are garbage: the caller restores them and redoes the N steps with
-// pll_step.  NaN anywhere reaches the phase accumulator and fails the final check.
-template <int N>
-FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], float (&out)[N], float Ki,
-                            float Kp, double step) {
+// pll_step.  NaN anywhere reaches the phase accumulator or the last trigArg and fails the
+// final check.
+//
+// The quotient without a reciprocal: with iv = (1/v)(1 + eta) and X = v (1 + delta),
+// |delta| <= 2^-23 (fc cs + fs sn = cs^2 + sn^2 + O(2^-24) for the floats fc, fs of the same
+// (cs, sn)), t = 2 - X iv = (1 - gamma), 1 + gamma = (1 + delta)(1 + eta), and
+// d = (Y iv) t = (Y / X)(1 - gamma^2): eta cancels to first order and the relative error is
+// gamma^2 + 3 roundings <= 2^-45, i.e. <= 2^-62 absolute for |d| < 2^-17 -- far inside E.
+//
+// The half turn of pll_offset for step j is 0.5 [v_j < 0] = 0.5 [iv_j < 0] (a NaN iv fails the
+// batch anyway).  refill(j) runs after step j, once the step has consumed v[j], iv[j] (and
+// iv[j + 1]'s sign) and pr[j]: the kernel reloads the next batch into the same registers from
+// there (one register set, the loads in flight for a whole batch).
+template <int N, class Refill>
+FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], const double (&iv)[N],
+                            const double (&pr)[N], float (&out)[N], float Ki, float Kp, Refill&& refill) {
     // undo the quadrant permutation: fc = [fbI, fbQ, -fbI, -fbQ][q], nfs = [-fbQ, fbI, fbQ, -fbI][q]
     const int q0 = ctx.q;
     const float u0 = (q0 & 1) ? p.fbQ : p.fbI, w0 = (q0 & 1) ? p.fbI : -p.fbQ;
     float fc = (q0 & 2) ? -u0 : u0, nfs = (q0 & 2) ? -w0 : w0;
     double cs = ctx.cs, sn = ctx.sn, x = ctx.x, nd = 0.0;
-    double B = pll_offset(x, v[0] < 0.0f ? 0.5 : 0.0);
+    double B = pll_offset_h(x, iv[0] < 0.0 ? 0.5 : 0.0);
     uint32_t acc_u = 0xFFFFFFFFu, acc_e = 0u;
-    double acc_d = 0.0, acc_B = fabs(B), acc_x = 0.0, acc_r = 1.0;
-    float acc_v = fabsf(v[0]);
+    double acc_d = 0.0, acc_B = fabs(B), acc_r = 1.0;
+    const bool range_ok = fabsf(p.phase) < kPllMaxPhase && fabsf(p.integ) < kPllMaxInteg;
 #ifdef __HIPCC__
 #pragma unroll
 #endif
     for (int j = 0; j < N; j++) {
+#ifdef __HIP_DEVICE_COMPILE__
+        const float2v ab = float2v{fc, nfs} * v[j];  // one v_pk_mul_f32
+        const float a = ab.x, b = ab.y;
+#else
         const float a = v[j] * fc, b = v[j] * nfs;
+#endif
         const double ad = (double)a, bd = (double)b;
         const double X = fma(ad, cs, -(bd * sn));
         const double Y = fma(ad, sn, bd * cs);
-        const double d = pll_quot(Y, X);
+        const double d = (Y * iv[j]) * fma(-X, iv[j], 2.0);
         const double th = d + B;
         const float lo = (float)(th - kPllE), hi = (float)(th + kPllE);
         acc_e |= __builtin_bit_cast(uint32_t, lo) ^ __builtin_bit_cast(uint32_t, hi);
         acc_d = fmax(acc_d, fabs(d));
         const float e = lo;
-        p.integ = p.integ + Ki * e;
-        p.phase = p.phase + ((Kp * e) + p.integ);
-        p.trig = p.trig + 1.0f;
-        const float arg = (float)(step * (double)p.trig + (double)p.phase);
+#ifdef __HIP_DEVICE_COMPILE__
+        const float2v ke = float2v{Ki, Kp} * e;  // one v_pk_mul_f32
+        const float ki_e = ke.x, kp_e = ke.y;
+#else
+        const float ki_e = Ki * e, kp_e = Kp * e;
+#endif
+        p.integ = p.integ + ki_e;
+        p.phase = p.phase + (kp_e + p.integ);
+        const float arg = (float)(pr[j] + (double)p.phase);
         out[j] = arg;
         x = (double)arg;
-        acc_x = fmax(acc_x, fabs(x));
         nd = rint(x * kInvPio2);
         const double r = fma(-nd, kPio2Lo, fma(-nd, kPio2Hi, x));
         acc_r = fmin(acc_r, fabs(r));
         pll_sincos_kernel(r, &sn, &cs);
         fc = (float)cs;
         nfs = -(float)sn;
-        const uint32_t mc = pll_margin16(cs), ms = pll_margin16(sn);
+        const uint32_t mc = pll_margin16x8(cs), ms = pll_margin16x8(sn);
         acc_u = acc_u < mc ? acc_u : mc;
         acc_u = acc_u < ms ? acc_u : ms;
         if (j + 1 < N) {
-            B = pll_offset(x, v[j + 1] < 0.0f ? 0.5 : 0.0);
+            B = pll_offset_h(x, iv[j + 1] < 0.0 ? 0.5 : 0.0);
             acc_B = fmax(acc_B, fabs(B));
-            acc_v = fminf(acc_v, fabsf(v[j + 1]));
         }
+        refill(j);
     }
+    // trigOffset after N float increments from an integer-valued trig in [0, 2^24] (the only
+    // case whose pr is not NaN)
+    p.trig = fminf(p.trig + (float)N, kPllTrigStick);
     // the quadrant permutation back: fbI = [fc, nfs, -fc, -nfs][q], fbQ = [-nfs, fc, nfs, -fc][q]
     const int q = (int)nd & 3;
     const float c1 = (q & 1) ? nfs : fc, s1 = (q & 1) ? fc : -nfs;
@@ -343,9 +409,9 @@ FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], float
     ctx.x = x;
     ctx.q = q;
     ctx.valid = true;
-    return (int)valid0 & (int)(acc_u > 32u) & (int)(acc_e == 0u) & (int)(acc_d < kPllMaxD) &
-           (int)(acc_B <= kPllMaxB) & (int)(acc_x < kPllMaxX) & (int)(acc_r >= kPllMinR) &
-           (int)(acc_v >= kPllMinV) & (int)(p.phase == p.phase);
+    return (int)valid0 & (int)range_ok & (int)(acc_u > 256u) & (int)(acc_e == 0u) &
+           (int)(acc_d < kPllMaxD) & (int)(acc_B <= kPllMaxB) & (int)(acc_r >= kPllMinR) &
+           (int)(p.phase == p.phase) & (int)(x == x);
 }
 
 }  // namespace fmrx

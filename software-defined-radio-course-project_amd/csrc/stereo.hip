@@ -10,6 +10,8 @@
 // place where the reference block size (SURVEY table M) changes the numbers.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "dsp_device.h"
 #include "fmrx_internal.h"
 #include "pll_math.h"
@@ -18,7 +20,6 @@ namespace fmrx {
 
 namespace {
 
-constexpr double kPi = 3.14159265358979323846;  // include/dy4.h:14
 constexpr int kBpMax = 64;
 
 struct BpTaps {
@@ -90,13 +91,57 @@ struct DeviceLib {
     }
 };
 
-constexpr int kPllBatch = 16;  // samples prefetched per batch (4 x 16-B loads)
+// Side data of one PLL segment (pll_math.h pll_side): iv, pr for every sample, in
+// parallel, from the trigOffset the segment starts with.  Two arrays of seg x n_streams
+// doubles, sample pairs stream-minor: element (j, s) at (j/2 * n_streams + s) * 2 + j%2, so
+// the PLL wave's lanes (one stream each) read consecutive 16-B pairs -- coalesced.
+__device__ inline size_t pll_side_at(int j, int s, int n_streams) {
+    return ((size_t)(j >> 1) * n_streams + s) * 2 + (j & 1);
+}
 
-__global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams, size_t stride, float freq, float fs,
-                           float norm_bw, float* st) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n_streams) return;
+__global__ void pll_prep_kernel(const float* io, int m, int n_streams, size_t stride, double* side, size_t seg,
+                                const float* st, double step) {
+    const int s = blockIdx.y;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const size_t a = pll_side_at(j, s, n_streams), rows = seg * (size_t)n_streams;
+    pll_side(io[(size_t)s * stride + j], st[8 * (size_t)s + 5], j, step, &side[a], &side[rows + a]);
+}
+
+// n exact steps (pll_step with the library fallbacks), out of line: the kernel then holds no
+// calls, so the batch loop's registers are not saved and restored around them.
+struct PllPair {
+    PllState p;
+    PllCtx ctx;
+};
+__device__ __noinline__ PllPair pll_redo(PllState p, PllCtx ctx, float* xb, int n, float Ki, float Kp, double step) {
+    const DeviceLib lib;
+#pragma unroll 1
+    for (int j = 0; j < n; j++) xb[j] = pll_step(p, ctx, xb[j], Ki, Kp, step, lib);
+    return PllPair{p, ctx};
+}
+
+// NB samples per optimistic batch.  Measured (10 s mode-0 stereo): NB = 16 beats 8 and 12.  The
+// certification is ~23 % of the step: without it the loop runs 0.31 s instead of 0.40 s.
+constexpr int kPllBatch = 16;
+//
+// Streams per wave (spw, a power of two <= 64): lane t works on stream blockIdx.x spw + t % spw,
+// and only lanes t < spw store.  The other lanes recompute their stream in lockstep (identical
+// values): a wave with every lane active runs the serial chain ~15 % faster than one with a
+// single live lane (one stream alone paid ~64 cycles a step of dependency stalls, a full wave
+// none), and up to one wave per SIMD the streams run side by side at that single-wave speed.
+template <int NB>
+__global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams, int spw, size_t stride,
+                                                 const double* side, size_t seg, double step, float norm_bw,
+                                                 float* st) {
+    const int s_lane = blockIdx.x * spw + (threadIdx.x & (spw - 1));
+    const bool owner = (int)threadIdx.x < spw && s_lane < n_streams;
+    const int s = s_lane < n_streams ? s_lane : n_streams - 1;
     float* x = io + (size_t)s * stride;
+    // pair q of batch b of this stream: element (b NB/2 + q) n_streams + s of a row of double2
+    // (uniform base + lane offset: global loads with an SGPR base, no per-load address VALU)
+    const double2* siv = reinterpret_cast<const double2*>(side);
+    const double2* spr = siv + seg * (size_t)n_streams / 2;
     float* S = st + 8 * (size_t)s;
     const float Cp = static_cast<float>(2.666);
     const float Ci = static_cast<float>(3.555);
@@ -105,54 +150,71 @@ __global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams
     PllState p{S[0], S[1], S[2], S[3], S[5]};
     PllCtx ctx{};
     ctx.valid = false;
-    const DeviceLib lib;
-    const double step = (2.0 * kPi) * static_cast<double>(freq / fs);
     int i = 0;
     if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
-        // Batches of 16 samples in two register sets used alternately (A: even batches, B:
-        // odd), each loaded a whole batch before its use: with one set copied forward the
-        // compiler waits for the next batch's loads (and the stores) at the top of every
-        // batch, exposing a memory round trip per 16 steps.
-        float A[kPllBatch], B[kPllBatch];
-        const int nb = n / kPllBatch;
-        auto load = [&](float (&dst)[kPllBatch], int b) {
-#pragma unroll
-            for (int q = 0; q < kPllBatch / 4; q++)
-                *reinterpret_cast<float4*>(&dst[4 * q]) = reinterpret_cast<const float4*>(x + b * kPllBatch)[q];
+        // Batches of NB samples + side data (v, iv, pr: 20 B a sample) in ONE register set:
+        // step j of batch b reloads the elements it has just consumed with batch b+1's (16-B
+        // loads; see pll_batch_fast's refill), so every load has a whole batch to land and no
+        // second set is needed (two sets overflow the 256 addressable VGPRs into AGPRs).
+        float v[NB];
+        double iv[NB], pr[NB];
+        const int nb = n / NB;
+        auto ld_v = [&](int b, int q) {  // floats 4q..4q+3
+            *reinterpret_cast<float4*>(&v[4 * q]) = reinterpret_cast<const float4*>(x + b * NB)[q];
         };
-        // Optimistic batches: the 16 steps run straight-line on the certified fast paths
-        // (pll_batch_fast: no per-step branch, no quadrant bookkeeping); only if some step of
-        // this stream could not be certified (~1e-4 per step) is the batch redone from the
-        // saved state on the exact path with the library fallbacks.  Bit-identical either way.
-        auto run = [&](float (&src)[kPllBatch], int b) {
+        auto ld_d = [&](double (&dst)[NB], const double2* row, int b, int q) {  // doubles 2q, 2q+1
+            *reinterpret_cast<double2*>(&dst[2 * q]) = (row + (size_t)(b * (NB / 2) + q) * n_streams)[s];
+        };
+        if (nb > 0) {
+#pragma unroll
+            for (int q = 0; q < NB / 4; q++) ld_v(0, q);
+#pragma unroll
+            for (int q = 0; q < NB / 2; q++) {
+                ld_d(iv, siv, 0, q);
+                ld_d(pr, spr, 0, q);
+            }
+        }
+        for (int b = 0; b < nb; b++) {
+            const int bn = b + 1 < nb ? b + 1 : b;  // the last batch reloads itself (no branch)
+            // after step j: v[j], pr[j] are dead, and iv[j] (its sign was read at step j-1)
+            auto refill = [&](int j) {
+                if (j % 4 == 3) ld_v(bn, j / 4);
+                if (j % 2 == 1) {
+                    ld_d(iv, siv, bn, j / 2);
+                    ld_d(pr, spr, bn, j / 2);
+                }
+            };
+            // Optimistic batch: the 16 steps run straight-line on the certified fast paths
+            // (pll_batch_fast: no per-step branch, no quadrant bookkeeping, no reciprocal);
+            // only if some step of this stream could not be certified (~1e-4 per step) is the
+            // batch redone from the saved state on the exact path with the library fallbacks,
+            // from the inputs still in memory.  Bit-identical either way.
             const PllState p0 = p;
             const PllCtx ctx0 = ctx;
-            float o[kPllBatch];
-            if (pll_batch_fast(p, ctx, src, o, Ki, Kp, step)) {
+            float o[NB];
+            float* xb = x + b * NB;
+            if (pll_batch_fast(p, ctx, v, iv, pr, o, Ki, Kp, refill)) {
+                if (owner) {
 #pragma unroll
-                for (int q = 0; q < kPllBatch / 4; q++)
-                    reinterpret_cast<float4*>(x + b * kPllBatch)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
-            } else {  // rare: redo from the saved state on the exact path
-                p = p0;
-                ctx = ctx0;
-                float* xb = x + b * kPllBatch;
-#pragma unroll 1
-                for (int j = 0; j < kPllBatch; j++) xb[j] = pll_step(p, ctx, xb[j], Ki, Kp, step, lib);
+                    for (int q = 0; q < NB / 4; q++)
+                        reinterpret_cast<float4*>(xb)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
+                }
+            } else {  // rare: redo from the saved state on the exact path (duplicate lanes of the
+                      // last stream read and write its samples in lockstep, identical values)
+                const PllPair r = pll_redo(p0, ctx0, xb, NB, Ki, Kp, step);
+                p = r.p;
+                ctx = r.ctx;
             }
-        };
-        if (nb > 0) load(A, 0);
-        int b = 0;
-        for (; b + 1 < nb; b += 2) {
-            load(B, b + 1);
-            run(A, b);
-            if (b + 2 < nb) load(A, b + 2);
-            run(B, b + 1);
         }
-        if (b < nb) run(A, b);
-        i = nb * kPllBatch;
+        i = nb * NB;
     }
-    for (; i < n; i++) x[i] = pll_step(p, ctx, x[i], Ki, Kp, step, lib);
-    S[0] = p.integ; S[1] = p.phase; S[2] = p.fbI; S[3] = p.fbQ; S[5] = p.trig;
+    if (i < n) {  // tail (and unaligned streams): exact steps
+        const PllPair r = pll_redo(p, ctx, x + i, n - i, Ki, Kp, step);
+        p = r.p;
+    }
+    if (owner) {
+        S[0] = p.integ; S[1] = p.phase; S[2] = p.fbI; S[3] = p.fbQ; S[5] = p.trig;
+    }
 }
 
 // filter.cpp:170: ncoOut[i] = cos(trigArg * nocoScale + phaseAdjust), float arithmetic inside,
@@ -304,11 +366,35 @@ int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s) {
     return ok();
 }
 
+size_t pll_side_doubles(int n, int n_streams) {
+    const size_t seg = std::min<size_t>(((size_t)std::max(n, 0) + 15) / 16 * 16, kPllSeg);
+    return 2 * seg * (size_t)n_streams;
+}
+
+// The recurrence in segments of at most kPllSeg samples per stream: side data of the segment
+// (parallel), then the serial PLL over it; the state carries in st between launches, so the
+// segments chain exactly like one launch.  Then the NCO of every sample in parallel.
 int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
-               float nco_scale, float phase_adjust, float norm_bw, float* st, hipStream_t s) {
+               float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s) {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(pll_kernel, dim3((n_streams + 63) / 64), dim3(64), 0, s, io, n, n_streams,
-                       stride, freq, fs, norm_bw, st);
+    const size_t seg = pll_side_doubles(n, 1) / 2;
+    // one stream per wave while the waves fit one per SIMD, then more streams per wave
+    static const int n_simd = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return 4 * cus;
+    }();
+    int spw = 1;
+    while (spw < 64 && (long long)spw * n_simd < n_streams) spw *= 2;
+    // filter.cpp:163: 2*PI*(freq/Fs) in double from the float quotient (host == device IEEE)
+    const double step = (2.0 * 3.14159265358979323846) * static_cast<double>(freq / fs);  // dy4.h:14 PI
+    for (size_t off = 0; off < (size_t)n; off += seg) {
+        const int m = (int)std::min(seg, (size_t)n - off);
+        hipLaunchKernelGGL(pll_prep_kernel, dim3((m + 255) / 256, n_streams), dim3(256), 0, s, io + off, m, n_streams,
+                           stride, side, seg, st, step);
+        hipLaunchKernelGGL(pll_kernel<kPllBatch>, dim3((n_streams + spw - 1) / spw), dim3(64), 0, s, io + off, m,
+                           n_streams, spw, stride, side, seg, step, norm_bw, st);
+    }
     hipLaunchKernelGGL(pll_nco_kernel, dim3((n + 255) / 256, n_streams), dim3(256), 0, s, io, n,
                        stride, nco_scale, phase_adjust, st);
     return ok();

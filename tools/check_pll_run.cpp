@@ -1,8 +1,9 @@
 // tools/check_pll_run.cpp — run the whole PLL recurrence (src/filter.cpp:136-174) two ways on
 // the host and require bit-identical output: (a) the reference's arithmetic with glibc's
 // double atan2/cos/sin, (b) csrc/pll_math.h's pll_step (certified fast paths + glibc
-// fallbacks), (c) pll_kernel's schedule: 16-sample pll_batch_fast batches, a batch redone with
-// pll_step when it cannot be certified, the tail with pll_step -- the GPU's arithmetic.
+// fallbacks), (c) pll_kernel's schedule: side data per chunk (pll_side, as pll_prep_kernel),
+// 16-sample pll_batch_fast batches, a batch redone with pll_step when it cannot be certified,
+// the tail with pll_step -- the GPU's arithmetic.
 // Usage: check_pll_run <carrier.f32> <freq> <fs> [chunk]   (state carried across chunks)
 #include <cmath>
 #include <algorithm>
@@ -78,13 +79,20 @@ int main(int argc, char** argv) {
         const size_t c1 = std::min(x.size(), c0 + chunk);
         std::vector<float> out(c1 - c0);
         size_t i = c0;
+        // side data of the chunk, as pll_prep_kernel computes it from the entering trigOffset
+        std::vector<double> iv(c1 - c0), pr(c1 - c0);
+        for (size_t k = c0; k < c1; k++)
+            fmrx::pll_side(x[k], pb.trig, (long long)(k - c0), step, &iv[k - c0], &pr[k - c0]);
         for (; i + NB <= c1; i += NB) {
             float v[NB], o[NB];
+            double bi[NB], bp[NB];
             std::memcpy(v, &x[i], sizeof v);
+            std::memcpy(bi, &iv[i - c0], sizeof bi);
+            std::memcpy(bp, &pr[i - c0], sizeof bp);
             const fmrx::PllState p0 = pb;
             const fmrx::PllCtx ctx0 = ctx;
             batches++;
-            if (!fmrx::pll_batch_fast(pb, ctx, v, o, Ki, Kp, step)) {
+            if (!fmrx::pll_batch_fast(pb, ctx, v, bi, bp, o, Ki, Kp, [](int) {})) {
                 redone++;
                 pb = p0;
                 ctx = ctx0;
