@@ -95,17 +95,34 @@ struct DeviceLib {
 // parallel, from the trigOffset the segment starts with.  Two arrays of seg x n_streams
 // doubles, sample pairs stream-minor: element (j, s) at (j/2 * n_streams + s) * 2 + j%2, so
 // the PLL wave's lanes (one stream each) read consecutive 16-B pairs -- coalesced.
-__device__ inline size_t pll_side_at(int j, int s, int n_streams) {
-    return ((size_t)(j >> 1) * n_streams + s) * 2 + (j & 1);
-}
 
-__global__ void pll_prep_kernel(const float* io, int m, int n_streams, size_t stride, double* side, size_t seg,
-                                const float* st, double step) {
-    const int s = blockIdx.y;
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= m) return;
-    const size_t a = pll_side_at(j, s, n_streams), rows = seg * (size_t)n_streams;
-    pll_side(io[(size_t)s * stride + j], st[8 * (size_t)s + 5], j, step, &side[a], &side[rows + a]);
+// One workgroup per tile of kPrepS streams x kPrepJ samples, transposed through LDS: rows of
+// the stream-major input are read coalesced, the stream-minor pairs written coalesced.
+constexpr int kPrepS = 16, kPrepJ = 64;
+__global__ void __launch_bounds__(256) pll_prep_kernel(const float* io, int m, int n_streams, size_t stride,
+                                                       double* side, size_t seg, const float* st, double step) {
+    __shared__ double2 t_iv[kPrepJ / 2][kPrepS], t_pr[kPrepJ / 2][kPrepS];
+    const int j0 = blockIdx.x * kPrepJ, s0 = blockIdx.y * kPrepS;
+    for (int e = threadIdx.x; e < kPrepS * kPrepJ; e += blockDim.x) {
+        const int r = e / kPrepJ, c = e % kPrepJ, s = s0 + r, j = j0 + c;
+        double iv = 0.0, pr = 0.0;
+        if (s < n_streams && j < m) pll_side(io[(size_t)s * stride + j], st[8 * (size_t)s + 5], j, step, &iv, &pr);
+        double* a = reinterpret_cast<double*>(&t_iv[c >> 1][r]);
+        double* b = reinterpret_cast<double*>(&t_pr[c >> 1][r]);
+        a[c & 1] = iv;
+        b[c & 1] = pr;
+    }
+    __syncthreads();
+    double2* siv = reinterpret_cast<double2*>(side);
+    double2* spr = siv + seg * (size_t)n_streams / 2;
+    for (int e = threadIdx.x; e < kPrepS * kPrepJ / 2; e += blockDim.x) {
+        const int jp = e / kPrepS, r = e % kPrepS, s = s0 + r;
+        if (s < n_streams && j0 + 2 * jp < m) {
+            const size_t a = (size_t)(j0 / 2 + jp) * n_streams + s;
+            siv[a] = t_iv[jp][r];
+            spr[a] = t_pr[jp][r];
+        }
+    }
 }
 
 // n exact steps (pll_step with the library fallbacks), out of line: the kernel then holds no
@@ -303,9 +320,11 @@ __device__ inline AudioView view(const AudioLaunch& L, int s, int b) {
 constexpr int kTail = 64;  // mixer tail kept across calls (>= ceil((at-1)/up) + 1)
 
 __global__ void stereo_audio_kernel(AudioLaunch L) {
-    const int s = blockIdx.z;
-    const int b = blockIdx.y;
-    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    // grid.x = n_blocks x frame tiles (no 65,535 limit on the block count), grid.y = streams
+    const int ft = (L.frames_per_block + (int)blockDim.x - 1) / (int)blockDim.x;
+    const int s = blockIdx.y;
+    const int b = blockIdx.x / ft;
+    const int m = (blockIdx.x - b * ft) * blockDim.x + threadIdx.x;
     if (m >= L.frames_per_block) return;
     const AudioView cur = view(L, s, b);
     const AudioView prv = b > 0 ? view(L, s, b - 1) : cur;
@@ -327,6 +346,77 @@ __global__ void stereo_audio_kernel(AudioLaunch L) {
     L.pcm[2 * o] = quantize_s16(right);        // project.cpp:184-187 (R first)
     L.pcm[2 * o + 1] = quantize_s16(left);
     if (L.mono_out) L.mono_out[o] = mono;
+}
+
+// Modes 0/1 (up = 1): one workgroup per (block, stream).  The block's (demod, mixer) pairs sit in
+// LDS behind the histories of both resamplers -- (previous block's mixer, own demod tail), the
+// shared-audio_state quirk of project.cpp:146/172 -- so the mono and stereo LPF of a frame are
+// ONE packed FIR over one float2 array (v_pk_mul/v_pk_add, each lane an ascending-tap
+// sequential sum as filter.cpp:84-92), and the mono of each frame is computed once: the 5-frame
+// delay line reads it back from LDS.  Same arithmetic as stereo_audio_kernel.
+constexpr int kTileIf = 1024, kTileFrames = 256, kTileTaps = 64;
+
+__global__ void __launch_bounds__(128) stereo_audio_tile_kernel(AudioLaunch L) {
+    constexpr int kPer = kTileFrames / 128;    // frames per thread
+    __shared__ float2 X[kTileTaps + kTileIf];  // X[H + j]: (mono input, stereo input) at IF index j
+    __shared__ float C[kTileTaps], MO[kTileFrames];
+    const int s = blockIdx.y, b = blockIdx.x;
+    const int ipb = L.if_per_block, fpb = L.frames_per_block, at = L.at, H = at - 1;
+    const AudioView cur = view(L, s, b);
+    for (int i = threadIdx.x; i < ipb; i += blockDim.x) X[H + i] = make_float2(cur.d[i], mixer_at(cur, i));
+    if (b > 0) {
+        const AudioView prv = view(L, s, b - 1);
+        for (int i = threadIdx.x; i < H; i += blockDim.x)
+            X[i] = make_float2(mixer_at(prv, ipb - H + i), cur.d[ipb - H + i]);
+    } else {
+        for (int i = threadIdx.x; i < H; i += blockDim.x)
+            X[i] = make_float2(L.mix_tail[(size_t)s * kTail + kTail - H + i], cur.d[ipb - H + i]);
+    }
+    for (int i = threadIdx.x; i < at; i += blockDim.x) C[i] = L.audio_c[i];
+    __syncthreads();
+    float st[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const int m = threadIdx.x + 128 * k;
+        st[k] = 0.0f;
+        if (m < fpb) {
+            const float2* x = X + H + m * L.down;
+            float2v acc = {0.0f, 0.0f};
+            for (int i = 0; i < at; i++) {
+                const float2 v = x[-i];
+                const float2v p = float2v{v.x, v.y} * C[i];
+                acc = acc + p;
+            }
+            MO[m] = acc.x;
+            st[k] = acc.y;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const int m = threadIdx.x + 128 * k;
+        if (m >= fpb) continue;
+        float shift;  // project.cpp:152-159, 5-sample delay line
+        if (m >= kMonoDelay) {
+            shift = MO[m - kMonoDelay];
+        } else if (b > 0) {  // the previous block's last frames read only its own demod (host-checked)
+            const float* d = view(L, s, b - 1).d + (fpb - kMonoDelay + m) * L.down;
+            float a = 0.0f;
+            for (int i = 0; i < at; i++) {
+                const float p = C[i] * d[-i];
+                a = a + p;
+            }
+            shift = a;
+        } else {
+            shift = L.mono_state[(size_t)s * 8 + m];
+        }
+        const float left = half_of(shift + st[k]);   // filter.cpp:196
+        const float right = half_of(shift - st[k]);  // filter.cpp:197
+        const size_t o = ((size_t)s * L.n_blocks + b) * (size_t)fpb + m;
+        L.pcm[2 * o] = quantize_s16(right);          // project.cpp:184-187 (R first)
+        L.pcm[2 * o + 1] = quantize_s16(left);
+        if (L.mono_out) L.mono_out[o] = MO[m];
+    }
 }
 
 // Carry the audio state of the LAST block of this call into the next call.
@@ -390,8 +480,8 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     const double step = (2.0 * 3.14159265358979323846) * static_cast<double>(freq / fs);  // dy4.h:14 PI
     for (size_t off = 0; off < (size_t)n; off += seg) {
         const int m = (int)std::min(seg, (size_t)n - off);
-        hipLaunchKernelGGL(pll_prep_kernel, dim3((m + 255) / 256, n_streams), dim3(256), 0, s, io + off, m, n_streams,
-                           stride, side, seg, st, step);
+        hipLaunchKernelGGL(pll_prep_kernel, dim3((m + kPrepJ - 1) / kPrepJ, (n_streams + kPrepS - 1) / kPrepS),
+                           dim3(256), 0, s, io + off, m, n_streams, stride, side, seg, st, step);
         hipLaunchKernelGGL(pll_kernel<kPllBatch>, dim3((n_streams + spw - 1) / spw), dim3(64), 0, s, io + off, m,
                            n_streams, spw, stride, side, seg, step, norm_bw, st);
     }
@@ -402,8 +492,14 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
 
 int launch_stereo_audio(const AudioLaunch& L, int n_streams, hipStream_t s) {
     if (L.n_blocks <= 0) return 0;
-    const dim3 grid((L.frames_per_block + 127) / 128, L.n_blocks, n_streams);
-    hipLaunchKernelGGL(stereo_audio_kernel, grid, dim3(128), 0, s, L);
+    const int H = L.at - 1;
+    if (L.up == 1 && L.if_per_block <= kTileIf && L.frames_per_block <= kTileFrames && L.at <= kTileTaps &&
+        L.frames_per_block * L.down <= L.if_per_block && (L.frames_per_block - kMonoDelay) * L.down >= H) {
+        hipLaunchKernelGGL(stereo_audio_tile_kernel, dim3(L.n_blocks, n_streams), dim3(128), 0, s, L);
+    } else {
+        const dim3 grid(((L.frames_per_block + 127) / 128) * L.n_blocks, n_streams);
+        hipLaunchKernelGGL(stereo_audio_kernel, grid, dim3(128), 0, s, L);
+    }
     hipLaunchKernelGGL(stereo_state_kernel, dim3(n_streams), dim3(kTail), 0, s, L);
     return ok();
 }
