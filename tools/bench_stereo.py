@@ -17,7 +17,12 @@ def main():
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--streams", type=int, nargs="+", default=[1, 32, 256])
     ap.add_argument("--mode", type=int, default=0)
+    ap.add_argument("--gib", action="store_true",
+                    help="BASELINE configs[2]: one stream of 1 GiB (83,886 mode-0 blocks) in ONE call, then the "
+                         "reference's own stereo path (oracle/_ref, 1 core) on the same bytes, PCM compared")
     args = ap.parse_args()
+    if args.gib:
+        return gib(args)
     import torch
     import iqgen
 
@@ -47,6 +52,44 @@ def main():
         rx.close()
         del iq, pcm
         torch.cuda.empty_cache()
+
+
+def gib(args):
+    import numpy as np
+    import torch
+
+    import iqgen
+
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    fm = iqgen.load_fmrx()
+    rx = fm.Receiver(args.mode, fm.STEREO)
+    bb = rx.geo.block_bytes
+    nb = (1 << 30) // bb
+    iq = torch.empty(nb * bb, dtype=torch.uint8, device="cuda")
+    pcm = torch.empty(nb * rx.geo.pcm_samples, dtype=torch.int16, device="cuda")
+    rx.synth_device(0, 0, nb * bb // 2, iq.data_ptr())
+    rx.synchronize()
+    t0 = time.perf_counter()
+    rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
+    rx.synchronize()
+    dt = time.perf_counter() - t0
+    sig = nb * bb / 2 / rx.geo.rf_fs
+    out = {"config": f"BASELINE configs[2]: mode-{args.mode} stereo, one stream, 1 GiB ({nb} blocks, {sig:.1f} s) "
+                     "in one call, device-resident", "seconds": round(dt, 3),
+           "MS_per_s": round(nb * bb / 2 / dt / 1e6, 1), "x_realtime": round(sig / dt, 1)}
+    if oracle.reference_available():
+        host = iq.cpu().numpy()
+        t0 = time.perf_counter()
+        ref = oracle.Reference().run(args.mode, 51, host, ["pcm"])["pcm"]
+        rdt = time.perf_counter() - t0
+        out["cpu_reference"] = {"seconds": round(rdt, 3), "x_realtime": round(sig / rdt, 1), "cores": 1,
+                                "kind": "reference", "what": "oracle/_ref sequential project.cpp stereo path "
+                                "(all stages, 1 core) on the same bytes"}
+        out["bit_exact_vs_reference"] = bool(np.array_equal(pcm.cpu().numpy(), ref))
+    print(json.dumps(out), flush=True)
+    rx.close()
 
 
 if __name__ == "__main__":
