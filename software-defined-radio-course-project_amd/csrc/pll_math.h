@@ -161,6 +161,7 @@ FMRX_HD bool fast_atan2_f(float yf, float xf, float* out) {
 
 constexpr double kInv2Pi = 1.59154943091895345608e-01;  // 1 / (2 pi)
 constexpr double kPllE = 4.0e-15;                       // absolute error bound of th
+constexpr double kPllEBatch = 2.0e-14;                  // ... with d = Y / v (pll_batch_fast)
 constexpr double kPllMaxD = 0x1p-17;                    // |d|: atan(d) = d to 1.5e-16
 constexpr double kPiHi = 3.14159265358979311600e+00;
 constexpr double kPllMaxB = kPiHi - 0x1p-12;            // |B|: off the branch cut
@@ -328,12 +329,14 @@ FMRX_HD uint32_t pll_margin16x8(double v) {
 // pll_step.  NaN anywhere reaches the phase accumulator or the last trigArg and fails the
 // final check.
 //
-// The quotient without a reciprocal: with iv = (1/v)(1 + eta) and X = v (1 + delta),
-// |delta| <= 2^-23 (fc cs + fs sn = cs^2 + sn^2 + O(2^-24) for the floats fc, fs of the same
-// (cs, sn)), t = 2 - X iv = (1 - gamma), 1 + gamma = (1 + delta)(1 + eta), and
-// d = (Y iv) t = (Y / X)(1 - gamma^2): eta cancels to first order and the relative error is
-// gamma^2 + 3 roundings <= 2^-45, i.e. <= 2^-62 absolute for |d| < 2^-17 -- far inside E.
-//
+// The quotient without X: d = Y iv, iv = (1/v)(1 + eta) from the pre-pass.  With
+// a = fl(v fc), b = fl(v nfs) and fc, fs the floats of (cs, sn) (or glibc's, within an ulp),
+// X / v = cs^2 (1 + e_c + e_a) + sn^2 (1 + e_s + e_b) = 1 + delta, |delta| <= 2^-23, and
+// |Y / v| = |cs sn (e_c + e_a - e_s - e_b)| <= 2^-23, so |d| <= 2^-23 and
+// |Y iv - Y / X| <= |Y / v| (|delta| + |eta|) <= 2^-46 < 1.5e-14.  The batch's bound is E
+// (kPllE, the rotation's own budget) plus that term: kPllEBatch = 2e-14.  The wider interval
+// leaves about one step in 10^5 uncertified (redone exactly), and saves X, its product and the
+// correction of a full quotient -- three operations on the serial chain.
 // The half turn of pll_offset for step j is 0.5 [v_j < 0] = 0.5 [iv_j < 0] (a NaN iv fails the
 // batch anyway).  refill(j) runs after step j, once the step has consumed v[j], iv[j] (and
 // iv[j + 1]'s sign) and pr[j]: the kernel reloads the next batch into the same registers from
@@ -361,11 +364,10 @@ FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], const
         const float a = v[j] * fc, b = v[j] * nfs;
 #endif
         const double ad = (double)a, bd = (double)b;
-        const double X = fma(ad, cs, -(bd * sn));
         const double Y = fma(ad, sn, bd * cs);
-        const double d = (Y * iv[j]) * fma(-X, iv[j], 2.0);
+        const double d = Y * iv[j];
         const double th = d + B;
-        const float lo = (float)(th - kPllE), hi = (float)(th + kPllE);
+        const float lo = (float)(th - kPllEBatch), hi = (float)(th + kPllEBatch);
         acc_e |= __builtin_bit_cast(uint32_t, lo) ^ __builtin_bit_cast(uint32_t, hi);
         acc_d = fmax(acc_d, fabs(d));
         const float e = lo;
