@@ -252,17 +252,19 @@ def test_stereo_multistream(fmrx, orc):
         assert np.array_equal(out[s], orc.run(0, 51, iq, ["pcm"])["pcm"]), s
 
 
-@pytest.mark.parametrize("channels,n_streams", [(2, 70), (1, 130)])
+@pytest.mark.parametrize("channels,n_streams", [(2, 70), (1, 130), (2, 1100)])
 def test_many_streams_cross_wave_boundaries(fmrx, orc, channels, n_streams):
-    """More streams than a wave has lanes (the PLL runs one lane per stream; the fused
-    kernel's segments per stream shrink as streams grow), streams of different content."""
+    """Many streams of different content: the PLL runs one stream per wave until the streams
+    outnumber the SIMDs (1,024 on MI355X), then two or more per wave (1,100 streams: two per
+    wave, lanes split by stream); the fused kernel's segments per stream shrink as streams
+    grow."""
     nb, bb = 3, 12800
     recipes = [("synth:%d" if s % 3 else "rand:%d") % (200 + s) for s in range(n_streams)]
     ins = np.stack([iqgen.make(r, nb * bb) for r in recipes])
     with fmrx.Receiver(0, channels, n_streams=n_streams) as rx:
         out = rx.process(ins)
     field = "pcm" if channels == 2 else "pcm_mono"
-    for s in (0, 1, 63, 64, 65, n_streams - 1):
+    for s in sorted({0, 1, 63, 64, 65, n_streams // 2, n_streams // 2 + 1, n_streams - 2, n_streams - 1}):
         assert np.array_equal(out[s], orc.run(0, 51, ins[s], [field])[field]), s
 
 
