@@ -325,6 +325,35 @@ def test_primitives(fmrx, taps_golden):
         assert same(fi.cpu().numpy(), g["norm_out"][0::2]) and same(fq.cpu().numpy(), g["norm_out"][1::2])
 
 
+@pytest.mark.parametrize("trig,phase,freq,fs,n,offset", [
+    (0.0, 0.0, 19000, 240000, 4103, 0),              # n % 16 != 0: exact tail
+    (16777200.0, 0.25, 19000, 240000, 700, 0),       # trigOffset sticks at 2^24 inside a batch
+    (0.5, 0.0, 19000, 240000, 300, 0),               # non-integer trigOffset: exact path only
+    (3.0e7, 0.0, 19000, 240000, 300, 0),             # past 2^24: exact path only
+    (0.0, 6.0e8, 19000, 240000, 300, 0),             # |phaseEst| beyond the batch's range check
+    (0.0, 0.0, 114000, 240000, 2000, 0),             # RDS's 114 kHz loop
+    (0.0, 0.0, 19000, 35280000, 2000, 0),            # mode 2's upsampled fs (project.cpp:166)
+    (0.0, 0.0, 19000, 240000, 1000, 1),              # unaligned samples: exact path only
+])
+def test_pll_primitive_states(fmrx, orc, trig, phase, freq, fs, n, offset):
+    """fmrx_pll (filter.cpp:136-174) from states the optimistic batches must refuse or handle
+    at their edges (trigOffset saturation, non-integer or huge trigOffset, huge phase, tails,
+    unaligned input), against the oracle's PLL on the same state."""
+    rng = np.random.default_rng(int(trig) + n)
+    t = np.arange(n)
+    x = (0.1 * np.cos(2 * np.pi * freq / fs * t + 0.3) + 0.01 * rng.standard_normal(n)).astype(np.float32)
+    st0 = np.array([1e-4, phase, 0.6, 0.8, 1.0, trig], np.float32)
+    want_x, want_st = orc.pll(x, freq, fs, 2.0, 0.0, 0.01, st0)
+    with fmrx.Receiver(0, fmrx.STEREO) as rx:
+        buf = _d(np.concatenate([np.zeros(offset, np.float32), x]))
+        st = _d(st0)
+        torch.cuda.synchronize()
+        rx.pll(buf.data_ptr() + 4 * offset, n, freq, fs, 2.0, 0.0, 0.01, st.data_ptr())
+        rx.synchronize()
+        assert same(buf.cpu().numpy()[offset:], want_x)
+        assert same(st.cpu().numpy(), want_st)
+
+
 def test_quantize_and_elementwise(fmrx, orc):
     x = np.array([0, 1, -1, 1.99993896484375, 2, -2, 2.5, 1e6, -1e6, 1.4e5, np.inf, -np.inf, np.nan,
                   131071.99, -131072, 3.05e-5] * 4, np.float32)
