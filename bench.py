@@ -38,8 +38,7 @@ RF_TAPS = 101
 _VARIANTS = ["mono_fused_kernel<101,10,5,256,3,3>", "mono_fused_kernel<101,10,5,128,3,3>",
              "mono_fused_kernel<101,10,5,64,3,3>", "mono_fused_kernel<101,10,5,128,5,3>",
              "mono_fused_kernel<101,10,5,256,3,5>", "mono_fused_kernel<101,10,5,64,3,3,TR=1>",
-             "mono_fused_kernel<101,10,5,64,3,4,TR=1>", "mono_fused_kernel<101,10,5,64,3,4,TR=2>",
-             "mono_fused_kernel<101,10,5,64,3,4,TR=2,FMT=1>"]
+             "mono_fused_kernel<101,10,5,64,3,4,TR=1>"]
 
 
 def kernel_name() -> str:

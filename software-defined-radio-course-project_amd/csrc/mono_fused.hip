@@ -42,10 +42,6 @@ namespace {
 
 constexpr int kAudioTaps = 51;  // src/project.cpp:319 (modes 0 and 1: audio_interp = 1)
 constexpr int kAH = kAudioTaps - 1;
-#ifndef FMRX_SGPR_GROUPS
-#define FMRX_SGPR_GROUPS 16
-#endif
-constexpr int kSgprGroups = FMRX_SGPR_GROUPS;
 
 template <int T, int D, int AD, int NT, int R>
 struct MonoCfg {
@@ -109,15 +105,6 @@ __device__ inline float sbyte(uint32_t w) {
     return f;
 }
 
-// FMT = 1: the prefetch is a typed buffer load (8_8_8_8 USCALED): the texture path converts
-// the 4 bytes of a dword to 4 floats u, so staging is s = u - 128 as two packed adds instead of
-// a xor and four byte conversions per dword.
-typedef int fmt_rsrc_t __attribute__((ext_vector_type(4)));
-typedef float fmt_f4_t __attribute__((ext_vector_type(4)));
-__device__ fmt_f4_t fmt_load_u8x4(fmt_rsrc_t rsrc, int voffset, int soffset, int aux) __asm(
-    "llvm.amdgcn.raw.buffer.load.format.v4f32");
-constexpr uint32_t kFmtDword3 = 0xFACu | (2u << 12) | (10u << 15);  // dst_sel xyzw, USCALED, 8_8_8_8
-
 // ABL (timing ablations only, never selected in production): bit 1 skips the RF FIR, 2 the
 // audio FIR, 4 the demod, 8 the byte conversion of the staging, 16 the global loads, 32 the
 // staging writes.
@@ -130,7 +117,7 @@ constexpr uint32_t kFmtDword3 = 0xFACu | (2u << 12) | (10u << 15);  // dst_sel x
 // SIMD, the audio FIR pipelined into the RF tap loop, staggered workgroup starts.
 // AU > 1: the audio stage is the rational resampler of modes 2/3 (up AU, down AD; 51 taps
 // per output phase of a 51*AU-tap prototype read from L.audio_coeff).
-template <int T, int D, int AD, int NT, int R, int PD, int ABL = 0, int TR = 0, int AU = 1, int FMT = 0>
+template <int T, int D, int AD, int NT, int R, int PD, int ABL = 0, int TR = 0, int AU = 1>
 __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps taps) {
     using C = MonoCfg<T, D, AD, NT, R>;
     constexpr int CIF = C::CIF, P = C::P, H = C::H, S = C::S, G = C::G, NLD = C::NLD;
@@ -188,17 +175,7 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     // the halo or run past the end (c outside [0, c_full)) are rebuilt at staging time.  One
     // load path keeps the loads asynchronous: with a second path the compiler merges the two
     // register sets right after issue, behind an s_waitcnt that exposes the HBM latency.
-    uint32_t pf[FMT ? 1 : NLD];
-    float pu[FMT ? 4 * NLD : 1];  // FMT: the prefetched bytes as floats u
-    // FMT: one buffer resource per segment, based at its first loaded chunk (offsets < 2^31)
-    const int cb = c0 > 0 ? c0 - 1 : 0;
-    fmt_rsrc_t rsrc{};
-    if constexpr (FMT != 0) {
-        const uint64_t a = reinterpret_cast<uint64_t>(in + (size_t)cb * (2 * P));
-        const long long left = total - (long long)cb * (2 * P);
-        rsrc = fmt_rsrc_t{(int)(uint32_t)a, (int)((uint32_t)(a >> 32) & 0xFFFFu),
-                          (int)(uint32_t)(left > 0xFFFFFFFFll ? 0xFFFFFFFFll : (left > 0 ? left : 0)), (int)kFmtDword3};
-    }
+    uint32_t pf[NLD];
     auto fetch = [&](int cc) {
         if constexpr ((ABL & 16) != 0) {  // ablation: no global loads
 #pragma unroll
@@ -207,19 +184,6 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         }
         if (c_full == 0) return;  // stream shorter than a chunk: every chunk is rebuilt
         const int cl = cc < 0 ? 0 : (cc < c_full ? cc : c_full - 1);
-        if constexpr (FMT != 0) {
-            const int vo = (cl - cb) * (2 * P) + 4 * tid;
-#pragma unroll
-            for (int l = 0; l < NLD; l++)
-                if ((P / 2) % NT == 0 || tid + l * NT < P / 2) {
-                    const fmt_f4_t f = fmt_load_u8x4(rsrc, vo + 4 * NT * l, 0, 0);
-                    pu[4 * l] = f.x;
-                    pu[4 * l + 1] = f.y;
-                    pu[4 * l + 2] = f.z;
-                    pu[4 * l + 3] = f.w;
-                }
-            return;
-        }
         const uint32_t* src = reinterpret_cast<const uint32_t*>(in + (size_t)cl * (2 * P)) + tid;
 #pragma unroll
         for (int l = 0; l < NLD; l++)
@@ -252,30 +216,12 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
 #pragma unroll
             for (int l = 0; l < NLD; l++) {
                 const int u = tid + l * NT;
-                if ((P / 2) % NT == 0 || u < P / 2) {
-                    const uint32_t w = load4(in, halo, (long long)c * (2 * P) + 4LL * u, total, hb);
-                    if constexpr (FMT != 0) {
-                        pu[4 * l] = (float)(w & 0xFFu);
-                        pu[4 * l + 1] = (float)((w >> 8) & 0xFFu);
-                        pu[4 * l + 2] = (float)((w >> 16) & 0xFFu);
-                        pu[4 * l + 3] = (float)(w >> 24);
-                    } else {
-                        pf[l] = w;
-                    }
-                }
+                if ((P / 2) % NT == 0 || u < P / 2) pf[l] = load4(in, halo, (long long)c * (2 * P) + 4LL * u, total, hb);
             }
         }
 #pragma unroll
         for (int l = 0; l < NLD; l++) {
             const int u = tid + l * NT;
-            if constexpr (FMT != 0) {  // s = u - 128, exact, two packed adds
-                if ((P / 2) % NT == 0 || u < P / 2) {
-                    const float2v lo = float2v{pu[4 * l], pu[4 * l + 1]} - 128.0f;
-                    const float2v hi = float2v{pu[4 * l + 2], pu[4 * l + 3]} - 128.0f;
-                    xb4[C::slot(H + 2 * u) / 2] = make_float4(lo.x, lo.y, hi.x, hi.y);
-                }
-                continue;
-            }
             if ((P / 2) % NT == 0 || u < P / 2) {
                 const uint32_t w = pf[l] ^ 0x80808080u;
                 if constexpr ((ABL & 32) != 0) {  // ablation: no staging writes
@@ -297,22 +243,11 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         // sum, while samples slide through a register window (each LDS pair read once per
         // thread).  Group 0 = tap 0, group j = taps 2j-1, 2j; group j's new samples are the
         // pair (T-1-2j, T-2j); loads run PD groups ahead of use.
-        if constexpr (TR == 1) {
+        if constexpr (TR != 0) {
             // Opaque per chunk, so LICM cannot hoist 101 loop-invariant (c, c) splats out of
             // the chunk loop; the products then broadcast a tap with op_sel instead.
 #pragma unroll
             for (int j = 0; j < NG; j++) asm volatile("" : "+v"(creg[j]));
-        }
-        if constexpr (TR == 2) {  // the first kSgprGroups tap groups in SGPRs, the rest in VGPRs
-#pragma unroll
-            for (int j = 0; j < NG; j++) {
-                if (j < kSgprGroups) {
-                    asm volatile("" : "+s"(creg[j].x));
-                    asm volatile("" : "+s"(creg[j].y));
-                } else {
-                    asm volatile("" : "+v"(creg[j]));
-                }
-            }
         }
         float2v acc[R];
 #pragma unroll
@@ -529,10 +464,10 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     }
 }
 
-template <int T, int D, int AD, int NT, int R, int PD, int TR = 0, int AU = 1, int FMT = 0>
+template <int T, int D, int AD, int NT, int R, int PD, int TR = 0, int AU = 1>
 int launch_variant(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStream_t s) {
-    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD, 0, TR, AU, FMT>), dim3(n_streams * L.segs), dim3(NT),
-                       0, s, L, taps);
+    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD, 0, TR, AU>), dim3(n_streams * L.segs), dim3(NT), 0,
+                       s, L, taps);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -542,8 +477,7 @@ struct Variant {
     int nt, r, pd, tr, wg_per_cu;  // wg_per_cu: resident workgroups per CU (LDS-limited)
 };
 constexpr Variant kVariants[] = {{256, 3, 3, 0, 2}, {128, 3, 3, 0, 4}, {64, 3, 3, 0, 8}, {128, 5, 3, 0, 3},
-                                 {256, 3, 5, 0, 2}, {64, 3, 3, 1, 8}, {64, 3, 4, 1, 8}, {64, 3, 4, 2, 8},
-                                 {64, 3, 4, 2, 8}};
+                                 {256, 3, 5, 0, 2}, {64, 3, 3, 1, 8}, {64, 3, 4, 1, 8}};
 constexpr int kDefaultVariant = 6;  // one wave per workgroup, taps in VGPRs, 4 groups of prefetch
 
 int variant_index() {  // FMRX_MONO_VARIANT: tuning sweeps only
@@ -632,10 +566,6 @@ int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_de
     FMRX_V(T_, D_, AD_, 6, 64, 3, 4, 1)
     FMRX_ALL(51, 10, 5)    // mode 0 (and mode 2's RF stage), reference taps
     FMRX_ALL(101, 10, 5)   // mode 0, 101-tap RF (BASELINE configs[1])
-    if (rf_taps == 101 && rf_decim == 10 && audio_down == 5 && vi == 7)
-        return launch_variant<101, 10, 5, 64, 3, 4, 2>(L, n_streams, taps, s);
-    if (rf_taps == 101 && rf_decim == 10 && audio_down == 5 && vi == 8)
-        return launch_variant<101, 10, 5, 64, 3, 4, 2, 1, 1>(L, n_streams, taps, s);
     FMRX_ALL(51, 4, 6)     // mode 1
     FMRX_ALL(101, 4, 6)
     // mode 3 (odd decimation 9): R = 2 keeps the per-thread stride S = 18 even; the
