@@ -86,6 +86,19 @@ int fmrx_state_size(const fmrx_ctx* ctx, size_t* bytes);
 int fmrx_get_state(fmrx_ctx* ctx, void* buf, size_t bytes);
 int fmrx_set_state(fmrx_ctx* ctx, const void* buf, size_t bytes);
 
+/* ---- time shards of one recording (mono product) ------------------------- */
+/* The mono product has finite memory: the RF FIR (rf_taps - 1 I/Q pairs), the demodulator's
+ * previous sample and the audio FIR depend only on a bounded run of raw bytes.  fmrx_seek
+ * makes the NEXT call continue a stream whose bytes before it are `prev` (per stream, the n
+ * bytes ending right before the call's first byte; stream-major, n_streams x n; n may be
+ * anything -- fewer than fmrx_history_bytes means the stream began inside them), so a shard
+ * of a recording that starts at a block boundary yields exactly the mono PCM the whole
+ * recording yields there.  prev_on_device: 0 host pointer, 1 device pointer.  MONO contexts
+ * only (the stereo PLL is a serial recurrence: FMRX_ESTATE); until the next fused call,
+ * fmrx_audio_block has no valid history and returns FMRX_ESTATE.                        */
+int fmrx_history_bytes(const fmrx_ctx* ctx, size_t* bytes);
+int fmrx_seek(fmrx_ctx* ctx, const uint8_t* prev, size_t n, int prev_on_device);
+
 /* ---- block-streaming entry points (host buffers; stream-major for n_streams > 1) ------ */
 /* iq: n_streams x (n_blocks * block_bytes) u8; pcm: n_streams x (n_blocks * pcm_samples).  */
 int fmrx_process(fmrx_ctx* ctx, const uint8_t* iq, size_t n_blocks, int16_t* pcm);

@@ -89,6 +89,7 @@ struct fmrx_ctx {
     // audio state of the mono product: last (audio_taps_total - 1) demod samples
     int audio_hist = 0;
     DevBuf<float> d_audio_hist;
+    bool audio_hist_stale = false;  // after fmrx_seek, until a fused call refreshes it
     // stereo engine state
     DevBuf<float> d_demod;        // n_streams x (kDemodHist + cap_if)
     size_t demod_stride = 0;
@@ -154,6 +155,7 @@ int reset_state(fmrx_ctx* c) {
     HIPCHK(hipMemsetAsync(c->d_halo[1].p, 0x80, c->halo_bytes * ns, c->stream));
     c->halo_cur = 0;
     HIPCHK(hipMemsetAsync(c->d_audio_hist.p, 0, sizeof(float) * c->audio_hist * ns, c->stream));
+    c->audio_hist_stale = false;
     if (c->d_demod.p)
         HIPCHK(hipMemsetAsync(c->d_demod.p, 0, sizeof(float) * c->d_demod.n, c->stream));
     // project.cpp:106-111: integrator 0, phaseEst 0, feedbackI 1, feedbackQ 0,
@@ -279,6 +281,7 @@ int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
                                c->geo.audio_up == 1 ? ad : c->geo.audio_down, c->mono_taps, c->stream);
     if (rc != 0) return fail(rc == -1 ? FMRX_EINVAL : FMRX_EHIP, "fused kernel launch failed (%d)", rc);
     if (ev) HIPCHK(hipEventRecord(ev->second, c->stream));
+    if (with_audio) c->audio_hist_stale = false;  // demod_tail rewrote the audio history
     rc = launch_halo_update(d_iq, L.stream_bytes, c->d_halo[c->halo_cur].p,
                             c->d_halo[c->halo_cur ^ 1].p, c->halo_bytes, ns, c->stream);
     if (rc != 0) return fail(FMRX_EHIP, "halo update failed");
@@ -529,6 +532,34 @@ void fmrx_destroy(fmrx_ctx* c) {
     delete c;
 }
 
+int fmrx_history_bytes(const fmrx_ctx* c, size_t* bytes) {
+    CtxLock lock_(c);
+    if (!c || !bytes) return fail(FMRX_EINVAL, "null argument");
+    *bytes = c->halo_bytes;
+    return FMRX_OK;
+}
+
+// The fused kernel rebuilds every float state of the mono product from the raw bytes in the
+// halo by a pre-roll chunk (mono_fused.hip), so seeking is setting the halo: the last
+// halo_bytes of prev, 0x80 (x = 0.0, the reference's zero-initialised state) in front of a
+// shorter prev.
+int fmrx_seek(fmrx_ctx* c, const uint8_t* prev, size_t n, int prev_on_device) {
+    CtxLock lock_(c);
+    if (!c || (!prev && n > 0)) return fail(FMRX_EINVAL, "bad argument");
+    if (c->cfg.channels != FMRX_MONO) return fail(FMRX_ESTATE, "fmrx_seek: mono product only (the PLL is serial)");
+    int rc = set_device(c);
+    if (rc) return rc;
+    const size_t ns = c->cfg.n_streams, hb = c->halo_bytes, m = std::min(n, hb);
+    uint8_t* h = c->d_halo[c->halo_cur].p;
+    if (m < hb) HIPCHK(hipMemset2DAsync(h, hb, 0x80, hb - m, ns, c->stream));
+    if (m > 0)
+        HIPCHK(hipMemcpy2DAsync(h + (hb - m), hb, prev + (n - m), n, m, ns,
+                                prev_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+    if (!prev_on_device) HIPCHK(hipStreamSynchronize(c->stream));  // prev may be freed on return
+    c->audio_hist_stale = true;
+    return FMRX_OK;
+}
+
 int fmrx_reset(fmrx_ctx* c) {
     CtxLock lock_(c);
     if (!c) return fail(FMRX_EINVAL, "null context");
@@ -597,7 +628,9 @@ int fmrx_get_state(fmrx_ctx* c, void* buf, size_t bytes) {
 int fmrx_set_state(fmrx_ctx* c, const void* buf, size_t bytes) {
     CtxLock lock_(c);
     if (!c || !buf) return fail(FMRX_EINVAL, "null argument");
-    return state_io(c, static_cast<uint8_t*>(const_cast<void*>(buf)), bytes, true);
+    const int rc = state_io(c, static_cast<uint8_t*>(const_cast<void*>(buf)), bytes, true);
+    if (rc == 0) c->audio_hist_stale = false;
+    return rc;
 }
 
 // ---- fused device-resident path ----------------------------------------------------------
@@ -703,6 +736,7 @@ int fmrx_audio_block(fmrx_ctx* c, const float* demod, size_t n_blocks, int16_t* 
     const size_t out_n = ns * n_blocks * c->geo.pcm_samples;
     if ((rc = c->d_out.ensure(out_n))) return rc;
     if (c->cfg.channels == FMRX_MONO) {
+        if (c->audio_hist_stale) return fail(FMRX_ESTATE, "no audio history after fmrx_seek (run a fused call first)");
         if ((rc = c->d_f32.ensure(ns * n_if))) return rc;
         HIPCHK(hipMemcpyAsync(c->d_f32.p, demod, sizeof(float) * ns * n_if, hipMemcpyHostToDevice, c->stream));
         if ((rc = run_mono_audio(c, c->d_f32.p, n_if, n_if, c->d_out.p, nullptr))) return rc;

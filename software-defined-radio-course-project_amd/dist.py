@@ -8,6 +8,12 @@ so that the collective moves equal-sized messages, and rank 0 drops the padding.
 The per-rank work is a callable ``process(stream_ids) -> tensor[len(ids), pcm_len]`` so the
 same sharding/gather code runs over libfmrx on GPUs (``fmrx_process_fn``) and, in the CPU
 tests, over the oracle with the gloo backend.
+
+ONE long recording can be cut in time instead (mono product only): rank r takes a
+contiguous range of blocks and seeks to the raw bytes in front of it (``fmrx_seek``: the mono
+product's state is a function of a bounded run of preceding bytes), so the gathered PCM is the
+whole recording's, bit for bit (``run_time_sharded``, ``fmrx_time_shard_fn``).  The stereo
+PLL is a serial recurrence: stereo streams are replicas only.
 """
 from __future__ import annotations
 
@@ -72,6 +78,45 @@ def fmrx_process_fn(fmrx, mode: int, channels: int, n_blocks: int, device: int, 
             for k, sid in enumerate(ids):
                 rx.synth_device(sid, 0, n_blocks * bb // 2, iq[k].data_ptr())
             rx.process_device(iq.data_ptr(), n_blocks, out.data_ptr())
+            rx.synchronize()
+            return out
+        finally:
+            rx.close()
+
+    return process
+
+
+def run_time_sharded(process: Callable[[range], torch.Tensor], n_blocks: int, pcm_per_block: int,
+                     world: int, rank: int) -> torch.Tensor | None:
+    """One stream cut in time: rank r processes blocks shard(n_blocks, world, r) (its
+    `process(blocks) -> tensor[len(blocks) * pcm_per_block]` seeks to the bytes in front of the
+    range first); rank 0 receives the whole stream's PCM, in order."""
+    blocks = shard(n_blocks, world, rank)
+    local = process(blocks)
+    assert local.shape == (len(blocks) * pcm_per_block,), (local.shape, len(blocks), pcm_per_block)
+    got = gather_pcm(local.view(len(blocks), pcm_per_block), n_blocks, pcm_per_block, world, rank)
+    return None if got is None else got.reshape(-1)
+
+
+def fmrx_time_shard_fn(fmrx, mode: int, seed: int, device: int, rf_taps: int = 51):
+    """GPU per-rank worker for run_time_sharded: the shard and the history bytes in front of it
+    are synthesized on the device (the generator is position-addressable), the context seeks to
+    the history, then processes the shard as one device-resident mono call."""
+
+    def process(blocks: range) -> torch.Tensor:
+        rx = fmrx.Receiver(mode, fmrx.MONO, rf_taps=rf_taps, device=device)
+        try:
+            bb, pcm = rx.geo.block_bytes, rx.geo.pcm_samples
+            out = torch.empty(len(blocks) * pcm, dtype=torch.int16, device=f"cuda:{device}")
+            if len(blocks) == 0:
+                return out
+            start = blocks.start * bb
+            pre = min(rx.history_bytes(), start)
+            buf = torch.empty(pre + len(blocks) * bb, dtype=torch.uint8, device=f"cuda:{device}")
+            torch.cuda.synchronize(device)
+            rx.synth_device(seed, (start - pre) // 2, buf.numel() // 2, buf.data_ptr())
+            rx.seek(buf.data_ptr(), pre)
+            rx.process_device(buf.data_ptr() + pre, len(blocks), out.data_ptr())
             rx.synchronize()
             return out
         finally:

@@ -56,6 +56,8 @@ PROTOTYPES = {
     "fmrx_state_size": (C.c_int, [_vp, C.POINTER(_sz)]),
     "fmrx_get_state": (C.c_int, [_vp, _vp, _sz]),
     "fmrx_set_state": (C.c_int, [_vp, _vp, _sz]),
+    "fmrx_history_bytes": (C.c_int, [_vp, C.POINTER(_sz)]),
+    "fmrx_seek": (C.c_int, [_vp, _vp, _sz, C.c_int]),
     "fmrx_process": (C.c_int, [_vp, _vp, _sz, _vp]),
     "fmrx_rf_block": (C.c_int, [_vp, _vp, _sz, _vp]),
     "fmrx_audio_block": (C.c_int, [_vp, _vp, _sz, _vp]),
@@ -294,6 +296,23 @@ class Receiver:
 
     def reset(self) -> None:
         _check(lib().fmrx_reset(self.h))
+
+    # ---- time shards of one recording (mono product)
+    def history_bytes(self) -> int:
+        """Raw bytes before a shard that fully determine the mono product's state there."""
+        n = C.c_size_t()
+        _check(lib().fmrx_history_bytes(self.h, C.byref(n)))
+        return n.value
+
+    def seek(self, prev, n: int | None = None) -> None:
+        """Continue, on the next call, a stream whose preceding bytes are `prev`: a host
+        array (n_streams x n u8, or 1-D for one stream) or, with `n` given, a device address
+        of n_streams x n bytes."""
+        if n is not None:
+            _check(lib().fmrx_seek(self.h, prev, n, 1))
+            return
+        a = np.ascontiguousarray(np.asarray(prev, np.uint8).reshape(self.cfg.n_streams, -1))
+        _check(lib().fmrx_seek(self.h, a.ctypes.data, a.shape[1], 0))
 
     # ---- filter.h primitives on device pointers
     def resample(self, d_out, d_state, d_in, n_in, d_coeff, taps, up, down) -> int:

@@ -1,5 +1,6 @@
-"""Worker for tests/test_distributed.py: one rank of the sharded multi-stream runner on CPU
-(gloo), with the oracle as the per-rank receiver.  Rank 0 saves the gathered PCM to argv[2]."""
+"""Worker for tests/test_distributed.py: one rank of the sharded multi-stream runner (or, with
+argv[3] == "time", of one stream cut in time) on CPU (gloo), with the oracle as the per-rank
+receiver.  Rank 0 saves the gathered PCM to argv[2]."""
 import os
 import sys
 
@@ -25,12 +26,36 @@ def process(ids):
     return torch.from_numpy(np.stack(rows))
 
 
+TIME_RECIPE = "synth:77"
+
+
+def process_time(n_blocks):
+    """One stream cut in time, the oracle as the receiver: it starts from the zero state, so
+    it is run from one whole block before the shard (more than the mono product's memory:
+    100 RF pairs + 50 demod samples) and that block's output is dropped -- the CPU analogue
+    of fmrx_seek."""
+    whole = iqgen.make(TIME_RECIPE, n_blocks * BB)
+
+    def process(blocks):
+        if len(blocks) == 0:
+            return torch.empty(0, dtype=torch.int16)
+        pre = min(1, blocks.start)
+        seg = whole[(blocks.start - pre) * BB: blocks.stop * BB]
+        pcm = oracle.Oracle().run(MODE, 51, seg, ["pcm_mono"])["pcm_mono"]
+        return torch.from_numpy(np.ascontiguousarray(pcm[pre * NA:]))
+
+    return process
+
+
 def main():
     n_streams, out_path = int(sys.argv[1]), sys.argv[2]
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     d = iqgen.load_module("dist")
-    got = d.run_sharded(process, n_streams, NB * NA * 2, world, rank)
+    if len(sys.argv) > 3 and sys.argv[3] == "time":  # argv[1] = blocks of the one stream
+        got = d.run_time_sharded(process_time(n_streams), n_streams, NA, world, rank)
+    else:
+        got = d.run_sharded(process, n_streams, NB * NA * 2, world, rank)
     if rank == 0:
         np.save(out_path, got.numpy())
     dist.destroy_process_group()

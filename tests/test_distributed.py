@@ -34,19 +34,33 @@ def test_shard_balanced_and_covering():
             assert max(map(len, rs)) - min(map(len, rs)) <= 1
 
 
-@pytest.mark.parametrize("n_streams", [5, 2, 1])
-def test_gather_world2_matches_serial(n_streams, orc, tmp_path):
+def _run_world2(tmp_path, *args):
     port = _free_port()
     out = tmp_path / "pcm.npy"
     procs = []
     for r in range(2):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
                    WORLD_SIZE="2", LOCAL_RANK=str(r))
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"),
-                                       str(n_streams), str(out)], env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"), str(args[0]),
+                                       str(out)] + [str(a) for a in args[1:]], env=env))
     for p in procs:
         assert p.wait(timeout=300) == 0
-    got = np.load(out)
+    return np.load(out)
+
+
+@pytest.mark.parametrize("n_streams", [5, 2, 1])
+def test_gather_world2_matches_serial(n_streams, orc, tmp_path):
+    got = _run_world2(tmp_path, n_streams)
     want = np.stack([orc.run(MODE, 51, iqgen.make(f"rand:{100 + i}", NB * BB), ["pcm"])["pcm"]
                      for i in range(n_streams)])
+    assert got.shape == want.shape and np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("n_blocks", [7, 2, 1])
+def test_time_shards_world2_match_whole_stream(n_blocks, orc, tmp_path):
+    """One recording cut in time over 2 ranks (dist.run_time_sharded): every rank restarts from
+    the bytes in front of its shard, and the gathered mono PCM equals the whole stream's."""
+    got = _run_world2(tmp_path, n_blocks, "time")
+    whole = iqgen.make("synth:77", n_blocks * BB)
+    want = orc.run(MODE, 51, whole, ["pcm_mono"])["pcm_mono"]
     assert got.shape == want.shape and np.array_equal(got, want)

@@ -161,6 +161,58 @@ def test_mono_multistream_independent(fmrx, orc):
         assert np.array_equal(out[s], orc.run(0, 101, iq, ["pcm_mono"])["pcm_mono"]), s
 
 
+@pytest.mark.parametrize("mode,rf_taps,nb,cuts", [(0, 101, 40, (1, 7, 23)), (0, 51, 12, (3,)),
+                                                   (1, 51, 30, (2, 17)), (2, 51, 4, (1, 3)), (3, 101, 3, (1, 2))])
+def test_time_shards_with_seek_equal_whole_stream(fmrx, mode, rf_taps, nb, cuts):
+    """fmrx_seek: a recording cut at block boundaries, each shard processed by a
+    fresh context that first seeks to the bytes in front of it (the whole prefix, or only the
+    last history_bytes of it), gives the whole recording's mono PCM bit for bit -- including
+    the first cut, whose prefix is shorter than the history (the stream began inside it)."""
+    bb, rf_fs = oracle.MODES[mode][0], oracle.MODES[mode][3]
+    iq = iqgen.make("synth:31", nb * bb, rf_fs)
+    with fmrx.Receiver(mode, fmrx.MONO, rf_taps=rf_taps) as rx:
+        whole = rx.process(iq)
+        hb = rx.history_bytes()
+    edges = [0, *cuts, nb]
+    for trim in (False, True):
+        pieces = []
+        for a, b in zip(edges, edges[1:]):
+            with fmrx.Receiver(mode, fmrx.MONO, rf_taps=rf_taps) as rx:
+                if a:
+                    prev = iq[: a * bb]
+                    rx.seek(prev[-hb:] if trim else prev)
+                pieces.append(rx.process(iq[a * bb: b * bb]))
+        assert np.array_equal(np.concatenate(pieces), whole), trim
+
+
+def test_time_shard_worker_and_seek_errors(fmrx):
+    """dist.fmrx_time_shard_fn (device-side history + seek) over 3 shards equals one context on
+    the whole stream; seek is refused for stereo and leaves the split API's audio stage
+    without history until a fused call."""
+    d = iqgen.load_module("dist")
+    nb, seed = 25, 4242
+    with fmrx.Receiver(0, fmrx.MONO) as rx:
+        bb, na = rx.geo.block_bytes, rx.geo.pcm_samples
+        iq = torch.empty(nb * bb, dtype=torch.uint8, device="cuda")
+        want = torch.empty(nb * na, dtype=torch.int16, device="cuda")
+        torch.cuda.synchronize()
+        rx.synth_device(seed, 0, nb * bb // 2, iq.data_ptr())
+        rx.process_device(iq.data_ptr(), nb, want.data_ptr())
+        rx.synchronize()
+    proc = d.fmrx_time_shard_fn(fmrx, 0, seed, 0)
+    got = torch.cat([proc(d.shard(nb, 3, r)) for r in range(3)])
+    assert torch.equal(got.cpu(), want.cpu())
+    with fmrx.Receiver(0, fmrx.STEREO) as rx:
+        with pytest.raises(RuntimeError):
+            rx.seek(np.zeros(100, np.uint8))
+    with fmrx.Receiver(0, fmrx.MONO) as rx:
+        rx.seek(np.full(64, 128, np.uint8))
+        with pytest.raises(RuntimeError):
+            rx.audio_block(np.zeros(640, np.float32))
+        rx.process(np.full(12800, 128, np.uint8))
+        rx.audio_block(np.zeros(640, np.float32))
+
+
 def test_partial_block_dropped_and_empty(fmrx, orc):
     iq = iqgen.make("synth:55", 3 * 12800 + 5000)
     with fmrx.Receiver(0, fmrx.MONO) as rx:
