@@ -57,6 +57,8 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-bytes", type=int, default=STREAM_BYTES)
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="skip the extra BASELINE configs (stereo 1 GiB, mode-2 mono) timed at N=1")
     args = ap.parse_args()
 
     import numpy as np
@@ -173,10 +175,66 @@ def main() -> None:
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the contract: rank 0 at N=1 only
         line["cpu_baseline"] = cpu_baseline(d_iq, d_pcm, args.cpu_sample_bytes, bb, na)
         line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(d_iq, args.cpu_sample_bytes, bb)
+    if world == 1 and not args.no_other_configs:
+        del d_iq, d_pcm
+        torch.cuda.empty_cache()
+        line["baseline_configs"] = other_configs(fmrx)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def other_configs(fmrx) -> dict:
+    """The other single-GPU BASELINE configs, timed on the same box (extra keys; `value` stays
+    configs[1]): configs[2] mode-0 stereo as ONE 1 GiB stream in one call (the serial PLL bounds
+    it), configs[3] mode-2 mono (147/800 resampler) over 1 GiB, device-resident, synthetic."""
+    import torch
+
+    out = {}
+    try:
+        rx = fmrx.Receiver(0, fmrx.STEREO)
+        bb = rx.geo.block_bytes
+        nb = STREAM_BYTES // bb
+        iq = torch.empty(nb * bb, dtype=torch.uint8, device="cuda")
+        pcm = torch.empty(nb * rx.geo.pcm_samples, dtype=torch.int16, device="cuda")
+        rx.synth_device(3000, 0, nb * bb // 2, iq.data_ptr())
+        rx.process_device(iq.data_ptr(), 16, pcm.data_ptr())  # warm-up, then from the start
+        rx.synchronize()
+        rx.reset()
+        t0 = time.perf_counter()
+        rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
+        rx.synchronize()
+        dt = time.perf_counter() - t0
+        sig = nb * bb / 2 / RT_RATE
+        out["configs[2]"] = {"workload": f"mode-0 stereo (REF_EXACT), one stream, 1 GiB ({nb} blocks) in one call",
+                             "seconds": round(dt, 3), "MS_per_s": round(nb * bb / 2 / dt / 1e6, 1),
+                             "x_realtime": round(sig / dt, 1)}
+        rx.close()
+        del iq, pcm
+        torch.cuda.empty_cache()
+        rx = fmrx.Receiver(2, fmrx.MONO)
+        bb = rx.geo.block_bytes
+        nb = STREAM_BYTES // bb
+        iq = torch.empty(nb * bb, dtype=torch.uint8, device="cuda")
+        pcm = torch.empty(nb * rx.geo.pcm_samples, dtype=torch.int16, device="cuda")
+        rx.synth_device(3001, 0, nb * bb // 2, iq.data_ptr())
+        for _ in range(2):
+            rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
+        rx.synchronize()
+        steps = 10
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
+        rx.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        out["configs[3]"] = {"workload": f"mode-2 mono, 147/800 polyphase resampler, 1 GiB ({nb} blocks)",
+                             "ms_per_step": round(dt * 1e3, 4), "MS_per_s": round(nb * bb / 2 / dt / 1e6, 1),
+                             "x_realtime": round(nb * bb / 2 / rx.geo.rf_fs / dt, 1)}
+        rx.close()
+    except Exception as e:  # the headline line must still print
+        out["error"] = repr(e)
+    return out
 
 
 def cpu_baseline(d_iq, d_pcm, sample_bytes, bb, na):

@@ -32,6 +32,9 @@ def test_bench_json_contract():
     assert j["n_gpus"] == 1 and j["steps"] == 2 and j["warmup"] == 1 and j["scaling"] == "weak"
     assert j["vs_baseline"] is None and j["higher_is_better"] is True
     assert "workload" in j["config"]
+    oc = j["baseline_configs"]  # the other single-GPU BASELINE configs, same box
+    assert "error" not in oc, oc
+    assert oc["configs[2]"]["x_realtime"] > 1 and oc["configs[3]"]["MS_per_s"] > 0
     rf = j["roofline"]
     assert rf["bound"] in ("hbm", "mfma") and rf["unit"] in ("GB/s", "TFLOP/s")
     assert 0 < rf["frac"] < 1 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
@@ -40,7 +43,7 @@ def test_bench_json_contract():
 
 
 def test_bench_cpu_baseline_keys():
-    j = _run("--cpu-sample-bytes", str(64 * 12800))
+    j = _run("--cpu-sample-bytes", str(64 * 12800), "--no-other-configs")
     cb = j["cpu_baseline"]
     assert cb["kind"] in ("reference", "port") and cb["cores"] == 1 and cb["value"] > 0
     assert cb["bit_exact_vs_gpu"] is True
