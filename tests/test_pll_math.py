@@ -50,9 +50,12 @@ def runner(tmp_path_factory):
     return exe
 
 
-@pytest.mark.parametrize("recipe,seconds,chunk", [("synth:5", 12.0, 640), ("rand:6", 3.0, 6400),
-                                                  ("const128", 0.5, 640), ("synth:8", 72.0, 1 << 30)])
-def test_pll_recurrence_bit_exact(runner, orc, tmp_path, recipe, seconds, chunk):
+@pytest.mark.parametrize("recipe,seconds,chunk,freq,fs", [
+    ("synth:5", 12.0, 640, 19000, 240000), ("rand:6", 3.0, 6400, 19000, 240000),
+    ("const128", 0.5, 640, 19000, 240000), ("synth:8", 72.0, 1 << 30, 19000, 240000),
+    ("synth:9", 6.0, 100003, 114000, 240000),      # the RDS loop's 114 kHz (project.cpp:259)
+    ("synth:9", 6.0, 100003, 19000, 35280000)])    # mode 2's upsampled fs (project.cpp:166)
+def test_pll_recurrence_bit_exact(runner, orc, tmp_path, recipe, seconds, chunk, freq, fs):
     """The whole PLL recurrence with the GPU's step function (rotation atan2 + certified
     sincos + fallbacks) equals the reference arithmetic bit for bit; the 72 s run crosses
     the float trigOffset saturation at 2^24 samples (69.9 s)."""
@@ -65,7 +68,7 @@ def test_pll_recurrence_bit_exact(runner, orc, tmp_path, recipe, seconds, chunk)
     carrier = orc.run(0, 51, iq, ["carrier"])["carrier"]
     f = tmp_path / "carrier.f32"
     carrier.astype(np.float32).tofile(f)
-    r = subprocess.run([runner, str(f), "19000", "240000", str(chunk)], capture_output=True, text=True,
+    r = subprocess.run([runner, str(f), str(freq), str(fs), str(chunk)], capture_output=True, text=True,
                        timeout=900)
     assert r.returncode == 0 and "mismatches=0 state_equal=1" in r.stdout, r.stdout
     # the GPU's optimistic 16-step batches are redone only rarely on real signals
