@@ -321,6 +321,51 @@ FMRX_HD uint32_t pll_margin16x8(double v) {
     return ((uint32_t)__builtin_bit_cast(uint64_t, v) << 3) + 0x80000080u;
 }
 
+// ---- sin and cos as ONE polynomial per lane (the batch's SPLIT form) -------------------------
+//
+// sin r = r (1 + z Ps(z)) and cos r = 1 + z (-1/2 + z Pc(z)), z = r^2, with fdlibm's
+// coefficients (Ps = S1 + S2 z + ... + S6 z^5, Pc = C1 + ... + C6 z^5), are the same seven-
+// coefficient Estrin evaluation Q(z) followed by w = 1 + z Q: sin lanes use q = (S1..S6, 0) and
+// take r w, cos lanes q = (-1/2, C1..C6) and take w.  On the device the even lanes of each
+// 16-lane row evaluate sin and the odd lanes cos with the SAME instructions, and two row
+// broadcasts (DPP row_newbcast: lane 0 = sin, lane 1 = cos) hand both to every lane of the row
+// -- five instructions fewer than evaluating both.  Error: Estrin ~1 ulp of Q, the fma and the
+// product 1/2 ulp each: <= 2.5 ulp relative (the 16-ulp margin test assumes <= 13.5).
+struct SplitCoef {
+    double q[7];
+};
+FMRX_HD SplitCoef split_coef(bool cos_lane) {
+    SplitCoef c;
+    const double s[7] = {kS1, kS2, kS3, kS4, kS5, kS6, 0.0};
+    const double k[7] = {-0.5, kC1, kC2, kC3, kC4, kC5, kC6};
+    for (int i = 0; i < 7; i++) c.q[i] = cos_lane ? k[i] : s[i];
+    return c;
+}
+FMRX_HD double split_w(double z, double z2, double z4, const SplitCoef& c) {
+    const double p01 = fma(z, c.q[1], c.q[0]), p23 = fma(z, c.q[3], c.q[2]), p45 = fma(z, c.q[5], c.q[4]);
+    const double Q = fma(z4, fma(z2, c.q[6], p45), fma(z2, p23, p01));
+    return fma(z, Q, 1.0);
+}
+// sin r, cos r in the split form: on the device lane_coef belongs to this lane (sin or cos by
+// lane parity) and the row broadcasts gather both; on the host both are evaluated.
+FMRX_HD void pll_sincos_split(double r, const SplitCoef& lane_coef, double* sn, double* cs) {
+    const double z = r * r, z2 = z * z, z4 = z2 * z2;
+#ifdef __HIP_DEVICE_COMPILE__
+    const double w = split_w(z, z2, z4, lane_coef);
+    const double rw = r * w;
+    const long long rw_bits = __builtin_bit_cast(long long, rw), w_bits = __builtin_bit_cast(long long, w);
+    // every lane of a row reads lane 0 / lane 1 of its row, so no lane keeps an old value
+    const long long sn_bits = __builtin_amdgcn_mov_dpp(rw_bits, 0x150, 0xF, 0xF, false);  // row_newbcast:0
+    const long long cs_bits = __builtin_amdgcn_mov_dpp(w_bits, 0x151, 0xF, 0xF, false);   // row_newbcast:1
+    *sn = __builtin_bit_cast(double, sn_bits);
+    *cs = __builtin_bit_cast(double, cs_bits);
+#else
+    (void)lane_coef;
+    *sn = r * split_w(z, z2, z4, split_coef(false));
+    *cs = split_w(z, z2, z4, split_coef(true));
+#endif
+}
+
 // N steps straight-line on the certified fast paths, with no branch and no quadrant work
 // (the representation above): the loop carries (fc, nfs, cs, sn, B) and folds every
 // certification into a few accumulators checked once at the end.  Returns true when every
@@ -341,9 +386,13 @@ FMRX_HD uint32_t pll_margin16x8(double v) {
 // batch anyway).  refill(j) runs after step j, once the step has consumed v[j], iv[j] (and
 // iv[j + 1]'s sign) and pr[j]: the kernel reloads the next batch into the same registers from
 // there (one register set, the loads in flight for a whole batch).
-template <int N, class Refill>
+//
+// SPLIT: sin/cos in the split form (pll_sincos_split; the device caller must run every lane of
+// a 16-lane row on the same stream, lane parity choosing `sc`).
+template <int N, bool SPLIT = false, class Refill>
 FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], const double (&iv)[N],
-                            const double (&pr)[N], float (&out)[N], float Ki, float Kp, Refill&& refill) {
+                            const double (&pr)[N], float (&out)[N], float Ki, float Kp, Refill&& refill,
+                            const SplitCoef& sc = SplitCoef{}) {
     // undo the quadrant permutation: fc = [fbI, fbQ, -fbI, -fbQ][q], nfs = [-fbQ, fbI, fbQ, -fbI][q]
     const int q0 = ctx.q;
     const float u0 = (q0 & 1) ? p.fbQ : p.fbI, w0 = (q0 & 1) ? p.fbI : -p.fbQ;
@@ -385,7 +434,10 @@ FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], const
         nd = rint(x * kInvPio2);
         const double r = fma(-nd, kPio2Lo, fma(-nd, kPio2Hi, x));
         acc_r = fmin(acc_r, fabs(r));
-        pll_sincos_kernel(r, &sn, &cs);
+        if constexpr (SPLIT)
+            pll_sincos_split(r, sc, &sn, &cs);
+        else
+            pll_sincos_kernel(r, &sn, &cs);
         fc = (float)cs;
         nfs = -(float)sn;
         const uint32_t mc = pll_margin16x8(cs), ms = pll_margin16x8(sn);

@@ -147,12 +147,18 @@ constexpr int kPllBatch = 16;
 // values): a wave with every lane active runs the serial chain ~15 % faster than one with a
 // single live lane (one stream alone paid ~64 cycles a step of dependency stalls, a full wave
 // none), and up to one wave per SIMD the streams run side by side at that single-wave speed.
-template <int NB>
+//
+// SPLIT (spw <= 4): streams by 16-lane row (lane t: stream blockIdx.x spw + (t / 16) % spw), so
+// the batch's sin and cos can be one polynomial per lane, even lanes sin, odd lanes cos, shared
+// by row broadcasts (pll_sincos_split); lane 0 of the stream's first row stores.
+template <int NB, bool SPLIT>
 __global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams, int spw, size_t stride,
                                                  const double* side, size_t seg, double step, float norm_bw,
                                                  float* st) {
-    const int s_lane = blockIdx.x * spw + (threadIdx.x & (spw - 1));
-    const bool owner = (int)threadIdx.x < spw && s_lane < n_streams;
+    const int t = threadIdx.x;
+    const int s_lane = blockIdx.x * spw + (SPLIT ? ((t >> 4) & (spw - 1)) : (t & (spw - 1)));
+    const bool owner = (SPLIT ? ((t & 15) == 0 && (t >> 4) < spw) : t < spw) && s_lane < n_streams;
+    const SplitCoef sc = split_coef((t & 1) != 0);
     const int s = s_lane < n_streams ? s_lane : n_streams - 1;
     float* x = io + (size_t)s * stride;
     // pair q of batch b of this stream: element (b NB/2 + q) n_streams + s of a row of double2
@@ -210,7 +216,7 @@ __global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams
             const PllCtx ctx0 = ctx;
             float o[NB];
             float* xb = x + b * NB;
-            if (pll_batch_fast(p, ctx, v, iv, pr, o, Ki, Kp, refill)) {
+            if (pll_batch_fast<NB, SPLIT>(p, ctx, v, iv, pr, o, Ki, Kp, refill, sc)) {
                 if (owner) {
 #pragma unroll
                     for (int q = 0; q < NB / 4; q++)
@@ -482,8 +488,12 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         const int m = (int)std::min(seg, (size_t)n - off);
         hipLaunchKernelGGL(pll_prep_kernel, dim3((m + kPrepJ - 1) / kPrepJ, (n_streams + kPrepS - 1) / kPrepS),
                            dim3(256), 0, s, io + off, m, n_streams, stride, side, seg, st, step);
-        hipLaunchKernelGGL(pll_kernel<kPllBatch>, dim3((n_streams + spw - 1) / spw), dim3(64), 0, s, io + off, m,
-                           n_streams, spw, stride, side, seg, step, norm_bw, st);
+        if (spw <= 4)
+            hipLaunchKernelGGL((pll_kernel<kPllBatch, true>), dim3((n_streams + spw - 1) / spw), dim3(64), 0, s,
+                               io + off, m, n_streams, spw, stride, side, seg, step, norm_bw, st);
+        else
+            hipLaunchKernelGGL((pll_kernel<kPllBatch, false>), dim3((n_streams + spw - 1) / spw), dim3(64), 0, s,
+                               io + off, m, n_streams, spw, stride, side, seg, step, norm_bw, st);
     }
     hipLaunchKernelGGL(pll_nco_kernel, dim3((n + 255) / 256, n_streams), dim3(256), 0, s, io, n,
                        stride, nco_scale, phase_adjust, st);

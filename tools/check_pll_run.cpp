@@ -4,7 +4,7 @@
 // fallbacks), (c) pll_kernel's schedule: side data per chunk (pll_side, as pll_prep_kernel),
 // 16-sample pll_batch_fast batches, a batch redone with pll_step when it cannot be certified,
 // the tail with pll_step -- the GPU's arithmetic.
-// Usage: check_pll_run <carrier.f32> <freq> <fs> [chunk]   (state carried across chunks)
+// Usage: check_pll_run <carrier.f32> <freq> <fs> [chunk] [split=1]   (state carried across chunks)
 #include <cmath>
 #include <algorithm>
 #include <cstdio>
@@ -36,6 +36,8 @@ int main(int argc, char** argv) {
     std::fclose(f);
     const float freq = std::atof(argv[2]), fs = std::atof(argv[3]);
     const size_t chunk = argc > 4 ? std::atol(argv[4]) : x.size();
+    // the GPU runs the split sin/cos form up to 4 streams per wave, the fdlibm form beyond
+    const bool split = argc > 5 ? std::atoi(argv[5]) != 0 : true;
     const float Kp = 0.01f * (float)2.666, Ki = (0.01f * 0.01f) * (float)3.555;
     const double step = (2.0 * 3.14159265358979323846) * (double)(freq / fs);
     // (a) reference arithmetic
@@ -92,7 +94,8 @@ int main(int argc, char** argv) {
             const fmrx::PllState p0 = pb;
             const fmrx::PllCtx ctx0 = ctx;
             batches++;
-            if (!fmrx::pll_batch_fast(pb, ctx, v, bi, bp, o, Ki, Kp, [](int) {})) {
+            if (!(split ? fmrx::pll_batch_fast<NB, true>(pb, ctx, v, bi, bp, o, Ki, Kp, [](int) {})
+                        : fmrx::pll_batch_fast<NB, false>(pb, ctx, v, bi, bp, o, Ki, Kp, [](int) {}))) {
                 redone++;
                 pb = p0;
                 ctx = ctx0;
