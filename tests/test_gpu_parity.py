@@ -304,12 +304,13 @@ def test_stereo_multistream(fmrx, orc):
         assert np.array_equal(out[s], orc.run(0, 51, iq, ["pcm"])["pcm"]), s
 
 
-@pytest.mark.parametrize("channels,n_streams", [(2, 70), (1, 130), (2, 1100)])
+@pytest.mark.parametrize("channels,n_streams", [(2, 70), (1, 130), (2, 1100), (2, 4200)])
 def test_many_streams_cross_wave_boundaries(fmrx, orc, channels, n_streams):
     """Many streams of different content: the PLL runs one stream per wave until the streams
-    outnumber the SIMDs (1,024 on MI355X), then two or more per wave (1,100 streams: two per
-    wave, lanes split by stream); the fused kernel's segments per stream shrink as streams
-    grow."""
+    outnumber the SIMDs (1,024 on MI355X), then two or four per wave with streams by 16-lane
+    row (the split sin/cos form; 1,100 streams), and beyond 4 per wave lanes split by stream
+    without it (4,200 streams: 8 per wave); the fused kernel's segments per stream shrink as
+    streams grow."""
     nb, bb = 3, 12800
     recipes = [("synth:%d" if s % 3 else "rand:%d") % (200 + s) for s in range(n_streams)]
     ins = np.stack([iqgen.make(r, nb * bb) for r in recipes])
