@@ -82,7 +82,7 @@ struct StereoLaunch {
 int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s);
 // PLL over n samples of n_streams streams (state st, 8 floats per stream), then the NCO
 // (filter.cpp:136-174).  side: device scratch of pll_side_doubles(n, n_streams) doubles.
-constexpr size_t kPllSeg = (size_t)1 << 18;  // samples per stream per PLL launch
+constexpr size_t kPllSeg = (size_t)1 << 18;  // at most this many samples per stream per PLL segment
 size_t pll_side_doubles(int n, int n_streams);
 int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
                float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s);

@@ -299,6 +299,23 @@ FMRX_HD bool pll_trig_domain(float t0) {
     return t0 >= 0.0f && t0 <= kPllTrigStick && t0 == floorf(t0);
 }
 
+// The state after step k - 1 of a segment (k >= 1 steps in) from what the speculative runner
+// records: (integ, phase) as recorded, trigOffset from the segment's integer-valued start t0
+// in the trig domain (min(t0 + k, 2^24), as pll_side), and fbI, fbQ -- not recorded -- rounded
+// from the exact sin/cos of that step's trigArg a (filter.cpp:166-169), which also leaves the
+// context for the next step.
+template <class Lib>
+FMRX_HD void pll_state_at(PllState& p, PllCtx& ctx, float integ, float phase, float t0, long long k, float a,
+                          const Lib& lib) {
+    p.integ = integ;
+    p.phase = phase;
+    p.trig = (float)fmin((double)t0 + (double)k, (double)kPllTrigStick);
+    float sv, cv;
+    if (!sincos_ctx_f(a, &sv, &cv, &ctx)) lib.sincosf_(a, &sv, &cv);
+    p.fbI = cv;
+    p.fbQ = sv;
+}
+
 FMRX_HD void pll_side(float v, float t0, long long j, double step, double* iv, double* pr) {
     const double vd = (double)v;
     *iv = (fabs(vd) >= (double)kPllMinV && fabs(vd) < 1.0e300) ? 1.0 / vd : (double)NAN;
@@ -389,7 +406,11 @@ FMRX_HD void pll_sincos_split(double r, const SplitCoef& lane_coef, double* sn, 
 //
 // SPLIT: sin/cos in the split form (pll_sincos_split; the device caller must run every lane of
 // a 16-lane row on the same stream, lane parity choosing `sc`).
-template <int N, bool SPLIT = false, class Refill>
+//
+// SPEC (the speculative runner, pll_spec_kernel): no certification at all -- e is the float
+// rounding of th and nothing is accumulated; the result is right unless a rounding went the
+// wrong way, which pll_check_kernel detects afterwards by recomputing every batch exactly.
+template <int N, bool SPLIT = false, bool SPEC = false, class Refill>
 FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], const double (&iv)[N],
                             const double (&pr)[N], float (&out)[N], float Ki, float Kp, Refill&& refill,
                             const SplitCoef& sc = SplitCoef{}) {
@@ -416,10 +437,15 @@ FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], const
         const double Y = fma(ad, sn, bd * cs);
         const double d = Y * iv[j];
         const double th = d + B;
-        const float lo = (float)(th - kPllEBatch), hi = (float)(th + kPllEBatch);
-        acc_e |= __builtin_bit_cast(uint32_t, lo) ^ __builtin_bit_cast(uint32_t, hi);
-        acc_d = fmax(acc_d, fabs(d));
-        const float e = lo;
+        float e;
+        if constexpr (SPEC) {
+            e = (float)th;
+        } else {
+            const float lo = (float)(th - kPllEBatch), hi = (float)(th + kPllEBatch);
+            acc_e |= __builtin_bit_cast(uint32_t, lo) ^ __builtin_bit_cast(uint32_t, hi);
+            acc_d = fmax(acc_d, fabs(d));
+            e = lo;
+        }
 #ifdef __HIP_DEVICE_COMPILE__
         const float2v ke = float2v{Ki, Kp} * e;  // one v_pk_mul_f32
         const float ki_e = ke.x, kp_e = ke.y;
@@ -433,19 +459,21 @@ FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], const
         x = (double)arg;
         nd = rint(x * kInvPio2);
         const double r = fma(-nd, kPio2Lo, fma(-nd, kPio2Hi, x));
-        acc_r = fmin(acc_r, fabs(r));
+        if constexpr (!SPEC) acc_r = fmin(acc_r, fabs(r));
         if constexpr (SPLIT)
             pll_sincos_split(r, sc, &sn, &cs);
         else
             pll_sincos_kernel(r, &sn, &cs);
         fc = (float)cs;
         nfs = -(float)sn;
-        const uint32_t mc = pll_margin16x8(cs), ms = pll_margin16x8(sn);
-        acc_u = acc_u < mc ? acc_u : mc;
-        acc_u = acc_u < ms ? acc_u : ms;
+        if constexpr (!SPEC) {
+            const uint32_t mc = pll_margin16x8(cs), ms = pll_margin16x8(sn);
+            acc_u = acc_u < mc ? acc_u : mc;
+            acc_u = acc_u < ms ? acc_u : ms;
+        }
         if (j + 1 < N) {
             B = pll_offset_h(x, iv[j + 1] < 0.0 ? 0.5 : 0.0);
-            acc_B = fmax(acc_B, fabs(B));
+            if constexpr (!SPEC) acc_B = fmax(acc_B, fabs(B));
         }
         refill(j);
     }
@@ -463,6 +491,7 @@ FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], const
     ctx.x = x;
     ctx.q = q;
     ctx.valid = true;
+    if constexpr (SPEC) return true;
     return (int)valid0 & (int)range_ok & (int)(acc_u > 256u) & (int)(acc_e == 0u) &
            (int)(acc_d < kPllMaxD) & (int)(acc_B <= kPllMaxB) & (int)(acc_r >= kPllMinR) &
            (int)(p.phase == p.phase) & (int)(x == x);

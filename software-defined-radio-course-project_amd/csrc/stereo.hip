@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "dsp_device.h"
 #include "fmrx_internal.h"
@@ -131,11 +132,19 @@ struct PllPair {
     PllState p;
     PllCtx ctx;
 };
-__device__ __noinline__ PllPair pll_redo(PllState p, PllCtx ctx, float* xb, int n, float Ki, float Kp, double step) {
+__device__ __noinline__ PllPair pll_redo(PllState p, PllCtx ctx, const float* xb, float* ob, int n, float Ki,
+                                         float Kp, double step) {
     const DeviceLib lib;
 #pragma unroll 1
-    for (int j = 0; j < n; j++) xb[j] = pll_step(p, ctx, xb[j], Ki, Kp, step, lib);
+    for (int j = 0; j < n; j++) ob[j] = pll_step(p, ctx, xb[j], Ki, Kp, step, lib);
     return PllPair{p, ctx};
+}
+
+// pll_math.h pll_state_at for the start of batch b (b NB steps into the segment), out of line.
+__device__ __noinline__ PllPair pll_state_at_batch(float2 rec, float t0, int b, int nbatch, float a) {
+    PllPair r;
+    pll_state_at(r.p, r.ctx, rec.x, rec.y, t0, (long long)b * nbatch, a, DeviceLib{});
+    return r;
 }
 
 // NB samples per optimistic batch.  Measured (10 s mode-0 stereo): NB = 16 beats 8 and 12.  The
@@ -151,16 +160,25 @@ constexpr int kPllBatch = 16;
 // SPLIT (spw <= 4): streams by 16-lane row (lane t: stream blockIdx.x spw + (t / 16) % spw), so
 // the batch's sin and cos can be one polynomial per lane, even lanes sin, odd lanes cos, shared
 // by row broadcasts (pll_sincos_split); lane 0 of the stream's first row stores.
+//
+// The exact PLL (and, after pll_spec_kernel / pll_check_kernel, the fix-up): trigArg of step j
+// goes to out[j] (out == io in place for the plain launch).  With `fail` (the first batch of
+// each stream whose speculative result did not verify, nb when all did), the wave starts at
+// the smallest such batch b0 of its streams, from the state recorded at the end of batch
+// b0 - 1 -- exact for every stream of the wave, since none failed before b0 -- so a segment
+// that verified costs only the tail.
 template <int NB, bool SPLIT>
 __global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams, int spw, size_t stride,
                                                  const double* side, size_t seg, double step, float norm_bw,
-                                                 float* st) {
+                                                 float* st, float* out_base, size_t ostride, const int* fail,
+                                                 const float2* rec, size_t rb) {
     const int t = threadIdx.x;
     const int s_lane = blockIdx.x * spw + (SPLIT ? ((t >> 4) & (spw - 1)) : (t & (spw - 1)));
     const bool owner = (SPLIT ? ((t & 15) == 0 && (t >> 4) < spw) : t < spw) && s_lane < n_streams;
     const SplitCoef sc = split_coef((t & 1) != 0);
     const int s = s_lane < n_streams ? s_lane : n_streams - 1;
     float* x = io + (size_t)s * stride;
+    float* out = out_base + (size_t)s * ostride;
     // pair q of batch b of this stream: element (b NB/2 + q) n_streams + s of a row of double2
     // (uniform base + lane offset: global loads with an SGPR base, no per-load address VALU)
     const double2* siv = reinterpret_cast<const double2*>(side);
@@ -174,6 +192,18 @@ __global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams
     PllCtx ctx{};
     ctx.valid = false;
     int i = 0;
+    int b0 = 0;
+    if (fail) {  // after the speculative runner: x is aligned (the host checked)
+        int m = fail[s];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o));
+        b0 = m;
+        if (b0 > 0) {
+            const PllPair r = pll_state_at_batch(rec[(size_t)s * rb + b0 - 1], p.trig, b0, NB, out[b0 * NB - 1]);
+            p = r.p;
+            ctx = r.ctx;
+        }
+    }
     if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
         // Batches of NB samples + side data (v, iv, pr: 20 B a sample) in ONE register set:
         // step j of batch b reloads the elements it has just consumed with batch b+1's (16-B
@@ -188,16 +218,16 @@ __global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams
         auto ld_d = [&](double (&dst)[NB], const double2* row, int b, int q) {  // doubles 2q, 2q+1
             *reinterpret_cast<double2*>(&dst[2 * q]) = (row + (size_t)(b * (NB / 2) + q) * n_streams)[s];
         };
-        if (nb > 0) {
+        if (b0 < nb) {
 #pragma unroll
-            for (int q = 0; q < NB / 4; q++) ld_v(0, q);
+            for (int q = 0; q < NB / 4; q++) ld_v(b0, q);
 #pragma unroll
             for (int q = 0; q < NB / 2; q++) {
-                ld_d(iv, siv, 0, q);
-                ld_d(pr, spr, 0, q);
+                ld_d(iv, siv, b0, q);
+                ld_d(pr, spr, b0, q);
             }
         }
-        for (int b = 0; b < nb; b++) {
+        for (int b = b0; b < nb; b++) {
             const int bn = b + 1 < nb ? b + 1 : b;  // the last batch reloads itself (no branch)
             // after step j: v[j], pr[j] are dead, and iv[j] (its sign was read at step j-1)
             auto refill = [&](int j) {
@@ -216,15 +246,16 @@ __global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams
             const PllCtx ctx0 = ctx;
             float o[NB];
             float* xb = x + b * NB;
+            float* ob = out + b * NB;
             if (pll_batch_fast<NB, SPLIT>(p, ctx, v, iv, pr, o, Ki, Kp, refill, sc)) {
                 if (owner) {
 #pragma unroll
                     for (int q = 0; q < NB / 4; q++)
-                        reinterpret_cast<float4*>(xb)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
+                        reinterpret_cast<float4*>(ob)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
                 }
             } else {  // rare: redo from the saved state on the exact path (duplicate lanes of the
                       // last stream read and write its samples in lockstep, identical values)
-                const PllPair r = pll_redo(p0, ctx0, xb, NB, Ki, Kp, step);
+                const PllPair r = pll_redo(p0, ctx0, xb, ob, NB, Ki, Kp, step);
                 p = r.p;
                 ctx = r.ctx;
             }
@@ -232,7 +263,7 @@ __global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams
         i = nb * NB;
     }
     if (i < n) {  // tail (and unaligned streams): exact steps
-        const PllPair r = pll_redo(p, ctx, x + i, n - i, Ki, Kp, step);
+        const PllPair r = pll_redo(p, ctx, x + i, out + i, n - i, Ki, Kp, step);
         p = r.p;
     }
     if (owner) {
@@ -240,15 +271,133 @@ __global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams
     }
 }
 
+// ---- speculative PLL: runner + parallel exact check + fix-up ---------------------------------
+//
+// The certification inside pll_batch_fast is ~20 % of the serial step.  pll_spec_kernel runs
+// the recurrence WITHOUT it (pll_batch_fast<SPEC>): trigArg to out, and (integ, phase) at the
+// end of every batch to rec.  pll_check_kernel then recomputes every batch of every stream in
+// parallel, one thread each, with the exact pll_step from the state the runner recorded at
+// the end of the previous batch (batch 0: the true initial state st), and compares the 16
+// trigArgs and the end state bit for bit; fail[s] = the first batch that differs.  By
+// induction every batch before fail[s] is exact.  pll_kernel (with `fail`) resumes from there
+// on the certified path and runs the tail, so the result equals the plain launch bit for bit
+// whatever the runner did; when everything verified it only runs the tail.
+template <int NB, bool SPLIT>
+__global__ void __launch_bounds__(64) pll_spec_kernel(const float* io, int n, int n_streams, int spw, size_t stride,
+                                                      const double* side, size_t seg, double step, float norm_bw,
+                                                      const float* st, float* out_base, size_t ostride, int* fail,
+                                                      float2* rec, size_t rb, int inject) {
+    const int t = threadIdx.x;
+    const int s_lane = blockIdx.x * spw + (SPLIT ? ((t >> 4) & (spw - 1)) : (t & (spw - 1)));
+    const bool owner = (SPLIT ? ((t & 15) == 0 && (t >> 4) < spw) : t < spw) && s_lane < n_streams;
+    const SplitCoef sc = split_coef((t & 1) != 0);
+    const int s = s_lane < n_streams ? s_lane : n_streams - 1;
+    const float* x = io + (size_t)s * stride;
+    float* out = out_base + (size_t)s * ostride;
+    const double2* siv = reinterpret_cast<const double2*>(side);
+    const double2* spr = siv + seg * (size_t)n_streams / 2;
+    const float* S = st + 8 * (size_t)s;
+    const float Kp = norm_bw * static_cast<float>(2.666);
+    const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
+    PllState p{S[0], S[1], S[2], S[3], S[5]};
+    const int nb = n / NB;
+    if (owner) fail[s] = nb;
+    // batch 0 on the exact path, as pll_kernel starts (a stream's first samples are often
+    // exact zeros, where the uncertified rotation is NaN), which also sets the context
+    PllCtx ctx{};
+    ctx.valid = false;
+    if (nb > 0) {
+        const PllPair r = pll_redo(p, ctx, x, out, NB, Ki, Kp, step);
+        p = r.p;
+        ctx = r.ctx;
+        if (owner) rec[(size_t)s * rb] = make_float2(p.integ, p.phase);
+    }
+    float v[NB];
+    double iv[NB], pr[NB];
+    auto ld_v = [&](int b, int q) {
+        *reinterpret_cast<float4*>(&v[4 * q]) = reinterpret_cast<const float4*>(x + b * NB)[q];
+    };
+    auto ld_d = [&](double (&dst)[NB], const double2* row, int b, int q) {
+        *reinterpret_cast<double2*>(&dst[2 * q]) = (row + (size_t)(b * (NB / 2) + q) * n_streams)[s];
+    };
+    if (nb > 1) {
+#pragma unroll
+        for (int q = 0; q < NB / 4; q++) ld_v(1, q);
+#pragma unroll
+        for (int q = 0; q < NB / 2; q++) {
+            ld_d(iv, siv, 1, q);
+            ld_d(pr, spr, 1, q);
+        }
+    }
+    for (int b = 1; b < nb; b++) {
+        const int bn = b + 1 < nb ? b + 1 : b;
+        auto refill = [&](int j) {
+            if (j % 4 == 3) ld_v(bn, j / 4);
+            if (j % 2 == 1) {
+                ld_d(iv, siv, bn, j / 2);
+                ld_d(pr, spr, bn, j / 2);
+            }
+        };
+        float o[NB];
+        (void)pll_batch_fast<NB, SPLIT, true>(p, ctx, v, iv, pr, o, Ki, Kp, refill, sc);
+        if (inject >= 0 && b == 1 + (inject + s) % (nb - 1)) p.phase += 1.0e-3f;  // test hook: a wrong batch
+        if (owner) {
+            float* ob = out + b * NB;
+#pragma unroll
+            for (int q = 0; q < NB / 4; q++)
+                reinterpret_cast<float4*>(ob)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
+            rec[(size_t)s * rb + b] = make_float2(p.integ, p.phase);
+        }
+    }
+}
+
+// One thread per (batch, stream): NB exact steps from the recorded start, compared bit for bit.
+template <int NB>
+__global__ void __launch_bounds__(64) pll_check_kernel(const float* io, int n, size_t stride, double step,
+                                                       float norm_bw, const float* st, const float* out_base,
+                                                       size_t ostride, int* fail, const float2* rec, size_t rb) {
+    const int s = blockIdx.y;
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nb = n / NB;
+    if (b >= nb) return;
+    const float* S = st + 8 * (size_t)s;
+    const float t0 = S[5];
+    if (!pll_trig_domain(t0)) {  // pll_state_at's trigOffset needs it: the whole segment exactly
+        if (b == 0) atomicMin(fail + s, 0);
+        return;
+    }
+    const float* x = io + (size_t)s * stride + (size_t)b * NB;
+    const float* o = out_base + (size_t)s * ostride + (size_t)b * NB;
+    const float Kp = norm_bw * static_cast<float>(2.666);
+    const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
+    PllState p{S[0], S[1], S[2], S[3], t0};
+    PllCtx ctx{};
+    ctx.valid = false;
+    if (b > 0) {
+        const PllPair r = pll_state_at_batch(rec[(size_t)s * rb + b - 1], t0, b, NB, o[-1]);
+        p = r.p;
+        ctx = r.ctx;
+    }
+    const DeviceLib lib;
+    bool same = true;
+    for (int j = 0; j < NB; j++) {
+        const float a = pll_step(p, ctx, x[j], Ki, Kp, step, lib);
+        same &= __float_as_uint(a) == __float_as_uint(o[j]);
+    }
+    const float2 e = rec[(size_t)s * rb + b];
+    same &= __float_as_uint(p.integ) == __float_as_uint(e.x) && __float_as_uint(p.phase) == __float_as_uint(e.y);
+    if (!same) atomicMin(fail + s, b);
+}
+
 // filter.cpp:170: ncoOut[i] = cos(trigArg * nocoScale + phaseAdjust), float arithmetic inside,
 // double cos, float result; also the ncoOut_state carry (filter.cpp:173).
-__global__ void pll_nco_kernel(float* io, int n, size_t stride, float nco_scale, float phase_adjust,
-                               float* st) {
+__global__ void pll_nco_kernel(float* io, int n, size_t stride, const float* args, size_t astride,
+                               float nco_scale, float phase_adjust, float* st) {
     const int s = blockIdx.y;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     float* x = io + (size_t)s * stride;
-    const float a = x[i] * nco_scale + phase_adjust;
+    const float a = args[(size_t)s * astride + i] * nco_scale + phase_adjust;
     float sv, cv;
     if (!fast_sincos_f(a, &sv, &cv)) cv = static_cast<float>(cos(static_cast<double>(a)));
     x[i] = cv;
@@ -462,41 +611,86 @@ int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s) {
     return ok();
 }
 
+// One segment's scratch, in doubles: the side data (iv, pr: 2 seg), the speculative runner's
+// trigArgs (seg floats), its batch records (seg / 16 float2) per stream, and fail[] (ints).
+// Segment length: kPllSeg samples up to 32 streams, then shorter so that segment x streams
+// stays ~2^23 (down to 2^14): a batch the runner got wrong (~3e-9 of steps) costs the rest
+// of its segment on the certified path, serially, so the expected cost per segment grows with
+// segment^2 x streams; launches per segment are ~4 (tens of microseconds).
+static size_t pll_seg_len(int n, int n_streams) {
+    size_t cap = kPllSeg;
+    while (cap > ((size_t)1 << 14) && cap * (size_t)std::max(n_streams, 1) > ((size_t)1 << 23)) cap >>= 1;
+    return std::min<size_t>(((size_t)std::max(n, 0) + 15) / 16 * 16, cap);
+}
 size_t pll_side_doubles(int n, int n_streams) {
-    const size_t seg = std::min<size_t>(((size_t)std::max(n, 0) + 15) / 16 * 16, kPllSeg);
-    return 2 * seg * (size_t)n_streams;
+    const size_t seg = pll_seg_len(n, n_streams);
+    return (2 * seg + seg / 2 + seg / kPllBatch) * (size_t)n_streams + ((size_t)n_streams + 1) / 2;
 }
 
 // The recurrence in segments of at most kPllSeg samples per stream: side data of the segment
 // (parallel), then the serial PLL over it; the state carries in st between launches, so the
-// segments chain exactly like one launch.  Then the NCO of every sample in parallel.
+// segments chain exactly like one launch.  Then the NCO of the segment's samples in parallel.
+// A segment runs speculatively (pll_spec_kernel, pll_check_kernel, then pll_kernel resuming at
+// the first batch that did not verify) unless FMRX_PLL_SPEC=0 or the streams' rows are not
+// 16-byte aligned; the plain path is pll_kernel in place.
 int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
                float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s) {
     if (n <= 0) return 0;
-    const size_t seg = pll_side_doubles(n, 1) / 2;
+    const size_t seg = pll_seg_len(n, n_streams);
+    const size_t rb = seg / kPllBatch;
+    float* args = reinterpret_cast<float*>(side + 2 * seg * (size_t)n_streams);  // seg per stream
+    float2* rec = reinterpret_cast<float2*>(args + seg * (size_t)n_streams);      // rb per stream
+    int* fail = reinterpret_cast<int*>(rec + rb * (size_t)n_streams);
     // one stream per wave while the waves fit one per SIMD, then more streams per wave
     static const int n_simd = [] {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         return 4 * cus;
     }();
+    const bool spec_env = [] {  // read per call: tests switch it within one process
+        const char* e = std::getenv("FMRX_PLL_SPEC");
+        return !(e && e[0] == '0');
+    }();
+    // test hook (tests/test_gpu_parity.py): the runner corrupts batch 1 + (k + s) % (nb - 1) of
+    // stream s, so the check and the fix-up from that batch run on every stream
+    const int inject = [] {
+        const char* e = std::getenv("FMRX_PLL_SPEC_INJECT");
+        return e ? std::atoi(e) : -1;
+    }();
+    const bool spec = spec_env && (reinterpret_cast<uintptr_t>(io) & 15) == 0 && stride % 4 == 0;
     int spw = 1;
     while (spw < 64 && (long long)spw * n_simd < n_streams) spw *= 2;
+    const dim3 grid((n_streams + spw - 1) / spw);
     // filter.cpp:163: 2*PI*(freq/Fs) in double from the float quotient (host == device IEEE)
     const double step = (2.0 * 3.14159265358979323846) * static_cast<double>(freq / fs);  // dy4.h:14 PI
     for (size_t off = 0; off < (size_t)n; off += seg) {
         const int m = (int)std::min(seg, (size_t)n - off);
+        float* x = io + off;
         hipLaunchKernelGGL(pll_prep_kernel, dim3((m + kPrepJ - 1) / kPrepJ, (n_streams + kPrepS - 1) / kPrepS),
-                           dim3(256), 0, s, io + off, m, n_streams, stride, side, seg, st, step);
+                           dim3(256), 0, s, x, m, n_streams, stride, side, seg, st, step);
+        float* out = spec ? args : x;
+        const size_t ostride = spec ? seg : stride;
+        if (spec) {
+            if (spw <= 4)
+                hipLaunchKernelGGL((pll_spec_kernel<kPllBatch, true>), grid, dim3(64), 0, s, x, m, n_streams, spw,
+                                   stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
+            else
+                hipLaunchKernelGGL((pll_spec_kernel<kPllBatch, false>), grid, dim3(64), 0, s, x, m, n_streams, spw,
+                                   stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
+            const int nb = m / kPllBatch;
+            if (nb > 0)
+                hipLaunchKernelGGL(pll_check_kernel<kPllBatch>, dim3((nb + 63) / 64, n_streams), dim3(64), 0, s, x, m,
+                                   stride, step, norm_bw, st, args, seg, fail, rec, rb);
+        }
         if (spw <= 4)
-            hipLaunchKernelGGL((pll_kernel<kPllBatch, true>), dim3((n_streams + spw - 1) / spw), dim3(64), 0, s,
-                               io + off, m, n_streams, spw, stride, side, seg, step, norm_bw, st);
+            hipLaunchKernelGGL((pll_kernel<kPllBatch, true>), grid, dim3(64), 0, s, x, m, n_streams, spw, stride,
+                               side, seg, step, norm_bw, st, out, ostride, spec ? fail : nullptr, rec, rb);
         else
-            hipLaunchKernelGGL((pll_kernel<kPllBatch, false>), dim3((n_streams + spw - 1) / spw), dim3(64), 0, s,
-                               io + off, m, n_streams, spw, stride, side, seg, step, norm_bw, st);
+            hipLaunchKernelGGL((pll_kernel<kPllBatch, false>), grid, dim3(64), 0, s, x, m, n_streams, spw, stride,
+                               side, seg, step, norm_bw, st, out, ostride, spec ? fail : nullptr, rec, rb);
+        hipLaunchKernelGGL(pll_nco_kernel, dim3((m + 255) / 256, n_streams), dim3(256), 0, s, x, m, stride, out,
+                           ostride, nco_scale, phase_adjust, st);
     }
-    hipLaunchKernelGGL(pll_nco_kernel, dim3((n + 255) / 256, n_streams), dim3(256), 0, s, io, n,
-                       stride, nco_scale, phase_adjust, st);
     return ok();
 }
 

@@ -321,6 +321,32 @@ def test_many_streams_cross_wave_boundaries(fmrx, orc, channels, n_streams):
         assert np.array_equal(out[s], orc.run(0, 51, ins[s], [field])[field]), s
 
 
+@pytest.mark.parametrize("env", [{"FMRX_PLL_SPEC": "0"}, {"FMRX_PLL_SPEC_INJECT": "0"},
+                                 {"FMRX_PLL_SPEC_INJECT": "7"}])
+@pytest.mark.parametrize("n_streams,nb", [(1, 450), (6, 40), (1100, 2)])
+def test_pll_speculation_fallbacks(fmrx, orc, monkeypatch, env, n_streams, nb):
+    """The speculative PLL (stereo.hip pll_spec_kernel -> pll_check_kernel -> pll_kernel from
+    the first batch that differs) equals the reference whatever the runner got wrong: with the
+    test hook FMRX_PLL_SPEC_INJECT=k the runner corrupts batch 1 + (k + s) % (nb - 1) of every
+    stream s, so every stream resumes at its own batch (and a wave of several streams, at 1,100
+    streams, at the earliest of them); FMRX_PLL_SPEC=0 is the plain certified launch.  450
+    blocks cross the 2^18-sample segment boundary."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    bb = 12800
+    recipes = [("synth:%d" if s % 3 else "rand:%d") % (900 + s) for s in range(n_streams)]
+    ins = np.stack([iqgen.make(r, nb * bb) for r in recipes])
+    with fmrx.Receiver(0, fmrx.STEREO, n_streams=n_streams) as rx:
+        out = np.atleast_2d(rx.process(ins))
+        if n_streams == 1:
+            out2 = np.atleast_2d(rx.process(ins))  # a second call from the carried state
+    for s in sorted({0, min(1, n_streams - 1), n_streams // 2, n_streams - 1}):
+        assert np.array_equal(out[s], orc.run(0, 51, ins[s], ["pcm"])["pcm"]), s
+    if n_streams == 1:
+        want2 = orc.run(0, 51, np.concatenate([ins[0], ins[0]]), ["pcm"])["pcm"][nb * 512 // 2:]
+        assert np.array_equal(out2[0], want2)
+
+
 @pytest.mark.parametrize("name", sorted(long_runs()))
 def test_stereo_long_hash(fmrx, name):
     h = long_runs()[name]

@@ -113,6 +113,97 @@ int main(int argc, char** argv) {
         }
     }
     state_ok = state_ok && pb.integ == integ && pb.phase == phase && pb.fbI == fbI && pb.fbQ == fbQ && pb.trig == trig;
+    // (d) the speculative launch (stereo.hip pll_spec_kernel / pll_check_kernel / pll_kernel
+    // with fail): the runner's uncertified batches with their (integ, phase) records, every
+    // batch rechecked with pll_step from the record before it, the certified path resumed at
+    // the first batch that differs, then the tail
+    fmrx::PllState ps{0, 0, 1, 0, 0};
+    size_t bad_d = 0, chunks = 0, chunks_failed = 0, batches_resumed = 0;
+    for (size_t c0 = 0; c0 < x.size(); c0 += chunk) {
+        const size_t c1 = std::min(x.size(), c0 + chunk), m = c1 - c0, nb = m / NB;
+        std::vector<double> iv(m), pr(m);
+        for (size_t k = c0; k < c1; k++) fmrx::pll_side(x[k], ps.trig, (long long)(k - c0), step, &iv[k - c0], &pr[k - c0]);
+        std::vector<float> out(m);
+        std::vector<std::pair<float, float>> rec(nb);
+        const fmrx::PllState s0 = ps;
+        {  // runner
+            fmrx::PllState p = s0;
+            fmrx::PllCtx ctx{};
+            ctx.valid = false;
+            if (nb > 0) {  // batch 0 exactly
+                for (int j = 0; j < NB; j++) out[j] = fmrx::pll_step(p, ctx, x[c0 + j], Ki, Kp, step, lib);
+                rec[0] = {p.integ, p.phase};
+            }
+            for (size_t b = 1; b < nb; b++) {
+                float v[NB], o[NB];
+                double bi[NB], bp[NB];
+                std::memcpy(v, &x[c0 + b * NB], sizeof v);
+                std::memcpy(bi, &iv[b * NB], sizeof bi);
+                std::memcpy(bp, &pr[b * NB], sizeof bp);
+                if (split) fmrx::pll_batch_fast<NB, true, true>(p, ctx, v, bi, bp, o, Ki, Kp, [](int) {});
+                else fmrx::pll_batch_fast<NB, false, true>(p, ctx, v, bi, bp, o, Ki, Kp, [](int) {});
+                std::memcpy(&out[b * NB], o, sizeof o);
+                rec[b] = {p.integ, p.phase};
+            }
+        }
+        size_t fail = nb;  // checker
+        for (size_t b = 0; b < nb; b++) {
+            fmrx::PllState p = s0;
+            fmrx::PllCtx ctx{};
+            ctx.valid = false;
+            if (!fmrx::pll_trig_domain(s0.trig)) { fail = 0; break; }
+            if (b > 0) fmrx::pll_state_at(p, ctx, rec[b - 1].first, rec[b - 1].second, s0.trig, (long long)(b * NB), out[b * NB - 1], lib);
+            bool same = true;
+            for (int j = 0; j < NB; j++) {
+                const float a = fmrx::pll_step(p, ctx, x[c0 + b * NB + j], Ki, Kp, step, lib);
+                same = same && std::memcmp(&a, &out[b * NB + j], 4) == 0;
+            }
+            same = same && std::memcmp(&p.integ, &rec[b].first, 4) == 0 && std::memcmp(&p.phase, &rec[b].second, 4) == 0;
+            if (!same) {
+                if (std::getenv("PLL_SPEC_VERBOSE")) std::printf("chunk at %zu: batch %zu of %zu differs\n", c0, b, nb);
+                fail = b;
+                break;
+            }
+        }
+        chunks++;
+        if (fail < nb) chunks_failed++;
+        batches_resumed += nb - fail;
+        {  // fix-up from batch `fail` on the certified path
+            fmrx::PllState p = s0;
+            fmrx::PllCtx ctx{};
+            ctx.valid = false;
+            if (fail > 0) fmrx::pll_state_at(p, ctx, rec[fail - 1].first, rec[fail - 1].second, s0.trig, (long long)(fail * NB), out[fail * NB - 1], lib);
+            size_t i = fail * NB;
+            for (; i + NB <= m; i += NB) {
+                float v[NB], o[NB];
+                double bi[NB], bp[NB];
+                std::memcpy(v, &x[c0 + i], sizeof v);
+                std::memcpy(bi, &iv[i], sizeof bi);
+                std::memcpy(bp, &pr[i], sizeof bp);
+                const fmrx::PllState p0 = p;
+                const fmrx::PllCtx ctx0 = ctx;
+                if (!(split ? fmrx::pll_batch_fast<NB, true>(p, ctx, v, bi, bp, o, Ki, Kp, [](int) {})
+                            : fmrx::pll_batch_fast<NB, false>(p, ctx, v, bi, bp, o, Ki, Kp, [](int) {}))) {
+                    p = p0;
+                    ctx = ctx0;
+                    for (int j = 0; j < NB; j++) o[j] = fmrx::pll_step(p, ctx, v[j], Ki, Kp, step, lib);
+                }
+                std::memcpy(&out[i], o, sizeof o);
+            }
+            for (; i < m; i++) out[i] = fmrx::pll_step(p, ctx, x[c0 + i], Ki, Kp, step, lib);
+            ps = p;
+        }
+        for (size_t k = c0; k < c1; k++) {
+            const float nco = (float)std::cos((double)(out[k - c0] * 2.0f + 0.0f));
+            if (std::memcmp(&nco, &ref[k], 4) != 0) {
+                if (bad_d < 5) std::printf("MISMATCH (speculative) at %zu: %.9g vs %.9g\n", k, nco, ref[k]);
+                bad_d++;
+            }
+        }
+    }
+    state_ok = state_ok && ps.integ == integ && ps.phase == phase && ps.fbI == fbI && ps.fbQ == fbQ && ps.trig == trig;
+    std::printf("speculative: chunks=%zu failed=%zu batches_resumed=%zu\n", chunks, chunks_failed, batches_resumed);
+    bad_c += bad_d;
     std::printf("batches=%zu redone=%zu\n", batches, redone);
     std::printf("samples=%zu mismatches=%zu state_equal=%d\n", x.size(), bad + bad_c, (int)state_ok);
     return (bad || bad_c || !state_ok) ? 1 : 0;
