@@ -413,13 +413,19 @@ FMRX_HD void pll_sincos_split(double r, const SplitCoef& lane_coef, double* sn, 
 template <int N, bool SPLIT = false, bool SPEC = false, class Refill>
 FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], const double (&iv)[N],
                             const double (&pr)[N], float (&out)[N], float Ki, float Kp, Refill&& refill,
-                            const SplitCoef& sc = SplitCoef{}) {
+                            const SplitCoef& sc = SplitCoef{}, const double* hh = nullptr) {
+    // hh (SPEC): the half turns 0.5 [v_j < 0] from the pre-pass, instead of a compare and a
+    // select per step
+    auto half = [&](int j) -> double {
+        if constexpr (SPEC) return hh[j];
+        return iv[j] < 0.0 ? 0.5 : 0.0;
+    };
     // undo the quadrant permutation: fc = [fbI, fbQ, -fbI, -fbQ][q], nfs = [-fbQ, fbI, fbQ, -fbI][q]
     const int q0 = ctx.q;
     const float u0 = (q0 & 1) ? p.fbQ : p.fbI, w0 = (q0 & 1) ? p.fbI : -p.fbQ;
     float fc = (q0 & 2) ? -u0 : u0, nfs = (q0 & 2) ? -w0 : w0;
     double cs = ctx.cs, sn = ctx.sn, x = ctx.x, nd = 0.0;
-    double B = pll_offset_h(x, iv[0] < 0.0 ? 0.5 : 0.0);
+    double B = pll_offset_h(x, half(0));
     uint32_t acc_u = 0xFFFFFFFFu, acc_e = 0u;
     double acc_d = 0.0, acc_B = fabs(B), acc_r = 1.0;
     const bool range_ok = fabsf(p.phase) < kPllMaxPhase && fabsf(p.integ) < kPllMaxInteg;
@@ -435,12 +441,12 @@ FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], const
 #endif
         const double ad = (double)a, bd = (double)b;
         const double Y = fma(ad, sn, bd * cs);
-        const double d = Y * iv[j];
-        const double th = d + B;
         float e;
         if constexpr (SPEC) {
-            e = (float)th;
+            e = (float)fma(Y, iv[j], B);  // one rounding fewer than d + B: no less accurate
         } else {
+            const double d = Y * iv[j];
+            const double th = d + B;
             const float lo = (float)(th - kPllEBatch), hi = (float)(th + kPllEBatch);
             acc_e |= __builtin_bit_cast(uint32_t, lo) ^ __builtin_bit_cast(uint32_t, hi);
             acc_d = fmax(acc_d, fabs(d));
@@ -472,7 +478,7 @@ FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], const
             acc_u = acc_u < ms ? acc_u : ms;
         }
         if (j + 1 < N) {
-            B = pll_offset_h(x, iv[j + 1] < 0.0 ? 0.5 : 0.0);
+            B = pll_offset_h(x, half(j + 1));
             if constexpr (!SPEC) acc_B = fmax(acc_B, fabs(B));
         }
         refill(j);

@@ -102,7 +102,7 @@ struct DeviceLib {
 constexpr int kPrepS = 16, kPrepJ = 64;
 __global__ void __launch_bounds__(256) pll_prep_kernel(const float* io, int m, int n_streams, size_t stride,
                                                        double* side, size_t seg, const float* st, double step) {
-    __shared__ double2 t_iv[kPrepJ / 2][kPrepS], t_pr[kPrepJ / 2][kPrepS];
+    __shared__ double2 t_iv[kPrepJ / 2][kPrepS], t_pr[kPrepJ / 2][kPrepS], t_h[kPrepJ / 2][kPrepS];
     const int j0 = blockIdx.x * kPrepJ, s0 = blockIdx.y * kPrepS;
     for (int e = threadIdx.x; e < kPrepS * kPrepJ; e += blockDim.x) {
         const int r = e / kPrepJ, c = e % kPrepJ, s = s0 + r, j = j0 + c;
@@ -110,18 +110,22 @@ __global__ void __launch_bounds__(256) pll_prep_kernel(const float* io, int m, i
         if (s < n_streams && j < m) pll_side(io[(size_t)s * stride + j], st[8 * (size_t)s + 5], j, step, &iv, &pr);
         double* a = reinterpret_cast<double*>(&t_iv[c >> 1][r]);
         double* b = reinterpret_cast<double*>(&t_pr[c >> 1][r]);
+        double* h = reinterpret_cast<double*>(&t_h[c >> 1][r]);
         a[c & 1] = iv;
         b[c & 1] = pr;
+        h[c & 1] = iv < 0.0 ? 0.5 : 0.0;  // pll_batch_fast's half turn (SPEC)
     }
     __syncthreads();
     double2* siv = reinterpret_cast<double2*>(side);
     double2* spr = siv + seg * (size_t)n_streams / 2;
+    double2* sh = spr + seg * (size_t)n_streams / 2;
     for (int e = threadIdx.x; e < kPrepS * kPrepJ / 2; e += blockDim.x) {
         const int jp = e / kPrepS, r = e % kPrepS, s = s0 + r;
         if (s < n_streams && j0 + 2 * jp < m) {
             const size_t a = (size_t)(j0 / 2 + jp) * n_streams + s;
             siv[a] = t_iv[jp][r];
             spr[a] = t_pr[jp][r];
+            sh[a] = t_h[jp][r];
         }
     }
 }
@@ -296,6 +300,7 @@ __global__ void __launch_bounds__(64) pll_spec_kernel(const float* io, int n, in
     float* out = out_base + (size_t)s * ostride;
     const double2* siv = reinterpret_cast<const double2*>(side);
     const double2* spr = siv + seg * (size_t)n_streams / 2;
+    const double2* sh = spr + seg * (size_t)n_streams / 2;
     const float* S = st + 8 * (size_t)s;
     const float Kp = norm_bw * static_cast<float>(2.666);
     const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
@@ -313,7 +318,7 @@ __global__ void __launch_bounds__(64) pll_spec_kernel(const float* io, int n, in
         if (owner) rec[(size_t)s * rb] = make_float2(p.integ, p.phase);
     }
     float v[NB];
-    double iv[NB], pr[NB];
+    double iv[NB], pr[NB], hh[NB];
     auto ld_v = [&](int b, int q) {
         *reinterpret_cast<float4*>(&v[4 * q]) = reinterpret_cast<const float4*>(x + b * NB)[q];
     };
@@ -327,6 +332,7 @@ __global__ void __launch_bounds__(64) pll_spec_kernel(const float* io, int n, in
         for (int q = 0; q < NB / 2; q++) {
             ld_d(iv, siv, 1, q);
             ld_d(pr, spr, 1, q);
+            ld_d(hh, sh, 1, q);
         }
     }
     for (int b = 1; b < nb; b++) {
@@ -336,10 +342,11 @@ __global__ void __launch_bounds__(64) pll_spec_kernel(const float* io, int n, in
             if (j % 2 == 1) {
                 ld_d(iv, siv, bn, j / 2);
                 ld_d(pr, spr, bn, j / 2);
+                ld_d(hh, sh, bn, j / 2);
             }
         };
         float o[NB];
-        (void)pll_batch_fast<NB, SPLIT, true>(p, ctx, v, iv, pr, o, Ki, Kp, refill, sc);
+        (void)pll_batch_fast<NB, SPLIT, true>(p, ctx, v, iv, pr, o, Ki, Kp, refill, sc, hh);
         if (inject >= 0 && b == 1 + (inject + s) % (nb - 1)) p.phase += 1.0e-3f;  // test hook: a wrong batch
         if (owner) {
             float* ob = out + b * NB;
@@ -611,7 +618,7 @@ int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s) {
     return ok();
 }
 
-// One segment's scratch, in doubles: the side data (iv, pr: 2 seg), the speculative runner's
+// One segment's scratch, in doubles: the side data (iv, pr, half turns: 3 seg), the speculative runner's
 // trigArgs (seg floats), its batch records (seg / 16 float2) per stream, and fail[] (ints).
 // Segment length: kPllSeg samples up to 32 streams, then shorter so that segment x streams
 // stays ~2^23 (down to 2^14): a batch the runner got wrong (~3e-9 of steps) costs the rest
@@ -624,7 +631,7 @@ static size_t pll_seg_len(int n, int n_streams) {
 }
 size_t pll_side_doubles(int n, int n_streams) {
     const size_t seg = pll_seg_len(n, n_streams);
-    return (2 * seg + seg / 2 + seg / kPllBatch) * (size_t)n_streams + ((size_t)n_streams + 1) / 2;
+    return (3 * seg + seg / 2 + seg / kPllBatch) * (size_t)n_streams + ((size_t)n_streams + 1) / 2;
 }
 
 // The recurrence in segments of at most kPllSeg samples per stream: side data of the segment
@@ -638,7 +645,7 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     if (n <= 0) return 0;
     const size_t seg = pll_seg_len(n, n_streams);
     const size_t rb = seg / kPllBatch;
-    float* args = reinterpret_cast<float*>(side + 2 * seg * (size_t)n_streams);  // seg per stream
+    float* args = reinterpret_cast<float*>(side + 3 * seg * (size_t)n_streams);  // seg per stream
     float2* rec = reinterpret_cast<float2*>(args + seg * (size_t)n_streams);      // rb per stream
     int* fail = reinterpret_cast<int*>(rec + rb * (size_t)n_streams);
     // one stream per wave while the waves fit one per SIMD, then more streams per wave

@@ -140,8 +140,10 @@ int main(int argc, char** argv) {
                 std::memcpy(v, &x[c0 + b * NB], sizeof v);
                 std::memcpy(bi, &iv[b * NB], sizeof bi);
                 std::memcpy(bp, &pr[b * NB], sizeof bp);
-                if (split) fmrx::pll_batch_fast<NB, true, true>(p, ctx, v, bi, bp, o, Ki, Kp, [](int) {});
-                else fmrx::pll_batch_fast<NB, false, true>(p, ctx, v, bi, bp, o, Ki, Kp, [](int) {});
+                double hh[NB];  // the pre-pass's half turns
+                for (int j = 0; j < NB; j++) hh[j] = bi[j] < 0.0 ? 0.5 : 0.0;
+                if (split) fmrx::pll_batch_fast<NB, true, true>(p, ctx, v, bi, bp, o, Ki, Kp, [](int) {}, {}, hh);
+                else fmrx::pll_batch_fast<NB, false, true>(p, ctx, v, bi, bp, o, Ki, Kp, [](int) {}, {}, hh);
                 std::memcpy(&out[b * NB], o, sizeof o);
                 rec[b] = {p.integ, p.phase};
             }
