@@ -130,6 +130,29 @@ __global__ void __launch_bounds__(256) pll_prep_kernel(const float* io, int m, i
     }
 }
 
+// The same side data stream-major (element (j, s) at s seg + j: each stream's samples
+// contiguous), for the split kernels: a wave there works on at most 4 streams, so stream-minor
+// rows would put every 16-B load of a wave on its own page (rows n_streams x 16 B apart).
+// One thread per sample pair.
+__global__ void __launch_bounds__(256) pll_prep_major_kernel(const float* io, int m, int n_streams, size_t stride,
+                                                             double* side, size_t seg, const float* st, double step) {
+    const int s = blockIdx.y;
+    const int jp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (2 * jp >= m) return;
+    const float t0 = st[8 * (size_t)s + 5];
+    double2 iv, pr, h;
+    pll_side(io[(size_t)s * stride + 2 * jp], t0, 2 * jp, step, &iv.x, &pr.x);
+    if (2 * jp + 1 < m) pll_side(io[(size_t)s * stride + 2 * jp + 1], t0, 2 * jp + 1, step, &iv.y, &pr.y);
+    else iv.y = pr.y = 0.0;
+    h.x = iv.x < 0.0 ? 0.5 : 0.0;
+    h.y = iv.y < 0.0 ? 0.5 : 0.0;
+    double2* siv = reinterpret_cast<double2*>(side);
+    const size_t plane = seg * (size_t)n_streams / 2, a = (size_t)s * (seg / 2) + jp;
+    siv[a] = iv;
+    siv[plane + a] = pr;
+    siv[2 * plane + a] = h;
+}
+
 // n exact steps (pll_step with the library fallbacks), out of line: the kernel then holds no
 // calls, so the batch loop's registers are not saved and restored around them.
 struct PllPair {
@@ -172,12 +195,13 @@ constexpr int kPllBatch = 16;
 // b0 - 1 -- exact for every stream of the wave, since none failed before b0 -- so a segment
 // that verified costs only the tail.
 template <int NB, bool SPLIT>
-__global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams, int spw, size_t stride,
+__global__ void __launch_bounds__(256) pll_kernel(float* io, int n, int n_streams, int spw, size_t stride,
                                                  const double* side, size_t seg, double step, float norm_bw,
                                                  float* st, float* out_base, size_t ostride, const int* fail,
                                                  const float2* rec, size_t rb) {
-    const int t = threadIdx.x;
-    const int s_lane = blockIdx.x * spw + (SPLIT ? ((t >> 4) & (spw - 1)) : (t & (spw - 1)));
+    const int t = threadIdx.x & 63;
+    const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int s_lane = wave * spw + (SPLIT ? ((t >> 4) & (spw - 1)) : (t & (spw - 1)));
     const bool owner = (SPLIT ? ((t & 15) == 0 && (t >> 4) < spw) : t < spw) && s_lane < n_streams;
     const SplitCoef sc = split_coef((t & 1) != 0);
     const int s = s_lane < n_streams ? s_lane : n_streams - 1;
@@ -220,7 +244,8 @@ __global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams
             *reinterpret_cast<float4*>(&v[4 * q]) = reinterpret_cast<const float4*>(x + b * NB)[q];
         };
         auto ld_d = [&](double (&dst)[NB], const double2* row, int b, int q) {  // doubles 2q, 2q+1
-            *reinterpret_cast<double2*>(&dst[2 * q]) = (row + (size_t)(b * (NB / 2) + q) * n_streams)[s];
+            *reinterpret_cast<double2*>(&dst[2 * q]) = SPLIT ? row[(size_t)s * (seg / 2) + b * (NB / 2) + q]
+                                                        : (row + (size_t)(b * (NB / 2) + q) * n_streams)[s];
         };
         if (b0 < nb) {
 #pragma unroll
@@ -287,12 +312,13 @@ __global__ void __launch_bounds__(64) pll_kernel(float* io, int n, int n_streams
 // on the certified path and runs the tail, so the result equals the plain launch bit for bit
 // whatever the runner did; when everything verified it only runs the tail.
 template <int NB, bool SPLIT>
-__global__ void __launch_bounds__(64) pll_spec_kernel(const float* io, int n, int n_streams, int spw, size_t stride,
+__global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, int n_streams, int spw, size_t stride,
                                                       const double* side, size_t seg, double step, float norm_bw,
                                                       const float* st, float* out_base, size_t ostride, int* fail,
                                                       float2* rec, size_t rb, int inject) {
-    const int t = threadIdx.x;
-    const int s_lane = blockIdx.x * spw + (SPLIT ? ((t >> 4) & (spw - 1)) : (t & (spw - 1)));
+    const int t = threadIdx.x & 63;
+    const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int s_lane = wave * spw + (SPLIT ? ((t >> 4) & (spw - 1)) : (t & (spw - 1)));
     const bool owner = (SPLIT ? ((t & 15) == 0 && (t >> 4) < spw) : t < spw) && s_lane < n_streams;
     const SplitCoef sc = split_coef((t & 1) != 0);
     const int s = s_lane < n_streams ? s_lane : n_streams - 1;
@@ -323,7 +349,8 @@ __global__ void __launch_bounds__(64) pll_spec_kernel(const float* io, int n, in
         *reinterpret_cast<float4*>(&v[4 * q]) = reinterpret_cast<const float4*>(x + b * NB)[q];
     };
     auto ld_d = [&](double (&dst)[NB], const double2* row, int b, int q) {
-        *reinterpret_cast<double2*>(&dst[2 * q]) = (row + (size_t)(b * (NB / 2) + q) * n_streams)[s];
+        *reinterpret_cast<double2*>(&dst[2 * q]) = SPLIT ? row[(size_t)s * (seg / 2) + b * (NB / 2) + q]
+                                                        : (row + (size_t)(b * (NB / 2) + q) * n_streams)[s];
     };
     if (nb > 1) {
 #pragma unroll
@@ -667,22 +694,30 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     const bool spec = spec_env && (reinterpret_cast<uintptr_t>(io) & 15) == 0 && stride % 4 == 0;
     int spw = 1;
     while (spw < 64 && (long long)spw * n_simd < n_streams) spw *= 2;
-    const dim3 grid((n_streams + spw - 1) / spw);
+    // Waves of 64 lanes; past 256 waves, workgroups of 4 waves, one per SIMD of a CU: 64-lane
+    // workgroups alone were placed two to a SIMD at 1,024 waves (half speed for both)
+    const int waves = (n_streams + spw - 1) / spw;
+    const int wpg = waves > n_simd / 4 ? 4 : 1;
+    const dim3 grid((waves + wpg - 1) / wpg), block(64 * wpg);
     // filter.cpp:163: 2*PI*(freq/Fs) in double from the float quotient (host == device IEEE)
     const double step = (2.0 * 3.14159265358979323846) * static_cast<double>(freq / fs);  // dy4.h:14 PI
     for (size_t off = 0; off < (size_t)n; off += seg) {
         const int m = (int)std::min(seg, (size_t)n - off);
         float* x = io + off;
-        hipLaunchKernelGGL(pll_prep_kernel, dim3((m + kPrepJ - 1) / kPrepJ, (n_streams + kPrepS - 1) / kPrepS),
-                           dim3(256), 0, s, x, m, n_streams, stride, side, seg, st, step);
+        if (spw <= 4)  // the split kernels read stream-major side data
+            hipLaunchKernelGGL(pll_prep_major_kernel, dim3(((m + 1) / 2 + 255) / 256, n_streams), dim3(256), 0, s, x, m,
+                               n_streams, stride, side, seg, st, step);
+        else
+            hipLaunchKernelGGL(pll_prep_kernel, dim3((m + kPrepJ - 1) / kPrepJ, (n_streams + kPrepS - 1) / kPrepS),
+                               dim3(256), 0, s, x, m, n_streams, stride, side, seg, st, step);
         float* out = spec ? args : x;
         const size_t ostride = spec ? seg : stride;
         if (spec) {
             if (spw <= 4)
-                hipLaunchKernelGGL((pll_spec_kernel<kPllBatch, true>), grid, dim3(64), 0, s, x, m, n_streams, spw,
+                hipLaunchKernelGGL((pll_spec_kernel<kPllBatch, true>), grid, block, 0, s, x, m, n_streams, spw,
                                    stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
             else
-                hipLaunchKernelGGL((pll_spec_kernel<kPllBatch, false>), grid, dim3(64), 0, s, x, m, n_streams, spw,
+                hipLaunchKernelGGL((pll_spec_kernel<kPllBatch, false>), grid, block, 0, s, x, m, n_streams, spw,
                                    stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
             const int nb = m / kPllBatch;
             if (nb > 0)
@@ -690,10 +725,10 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
                                    stride, step, norm_bw, st, args, seg, fail, rec, rb);
         }
         if (spw <= 4)
-            hipLaunchKernelGGL((pll_kernel<kPllBatch, true>), grid, dim3(64), 0, s, x, m, n_streams, spw, stride,
+            hipLaunchKernelGGL((pll_kernel<kPllBatch, true>), grid, block, 0, s, x, m, n_streams, spw, stride,
                                side, seg, step, norm_bw, st, out, ostride, spec ? fail : nullptr, rec, rb);
         else
-            hipLaunchKernelGGL((pll_kernel<kPllBatch, false>), grid, dim3(64), 0, s, x, m, n_streams, spw, stride,
+            hipLaunchKernelGGL((pll_kernel<kPllBatch, false>), grid, block, 0, s, x, m, n_streams, spw, stride,
                                side, seg, step, norm_bw, st, out, ostride, spec ? fail : nullptr, rec, rb);
         hipLaunchKernelGGL(pll_nco_kernel, dim3((m + 255) / 256, n_streams), dim3(256), 0, s, x, m, stride, out,
                            ostride, nco_scale, phase_adjust, st);
