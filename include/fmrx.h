@@ -130,7 +130,11 @@ int fmrx_resample(fmrx_ctx* ctx, float* d_out, float* d_state, const float* d_in
 int fmrx_fm_demod(fmrx_ctx* ctx, float* d_out, float* d_prev, const float* d_i,
                   const float* d_q, int n);
 /* d_io: PLL input, overwritten by the NCO output.  d_st: 6 floats {integrator, phaseEst,
- * feedbackI, feedbackQ, ncoOut_state, trigOffset} (in/out).                                */
+ * feedbackI, feedbackQ, ncoOut_state, trigOffset} (in/out).  Every PLL (this call, stereo,
+ * RDS) runs speculatively -- the serial loop without certification, every 16-sample batch
+ * re-verified exactly in parallel, the certified path from the first batch that differs --
+ * with the same bits either way; environment FMRX_PLL_SPEC=0 selects the plain certified
+ * launch.                                                                                  */
 int fmrx_pll(fmrx_ctx* ctx, float* d_io, int n, float freq, float fs, float nco_scale,
              float phase_adjust, float norm_bw, float* d_st);
 int fmrx_mixer(fmrx_ctx* ctx, float* d_out, const float* d_a, const float* d_b, int n);

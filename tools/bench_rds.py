@@ -40,7 +40,7 @@ def main():
         d_in = torch.from_numpy(np.tile(base, (ns, 1))).cuda()
         d_out = torch.empty_like(d_in)
         with fm.Receiver(args.mode, fm.STEREO, n_streams=ns) as rx:
-            rx.rds_device(d_in.data_ptr(), 1, d_out.data_ptr())  # warm-up (one block)
+            rx.rds_device(d_in.data_ptr(), nb, d_out.data_ptr())  # warm-up: code objects, buffers sized
             rx.synchronize()
             rx.reset()
             torch.cuda.synchronize()

@@ -37,7 +37,7 @@ def main():
         for s in range(ns):
             rx.synth_device(s, 0, nb * bb // 2, iq[s].data_ptr())
         rx.synchronize()
-        rx.process_device(iq.data_ptr(), 1, pcm.data_ptr())  # warm-up (1 block)
+        rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())  # warm-up: code objects, buffers sized
         rx.synchronize()
         rx.reset()
         t0 = time.perf_counter()
