@@ -389,7 +389,8 @@ __global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, i
 template <int NB>
 __global__ void __launch_bounds__(64) pll_check_kernel(const float* io, int n, size_t stride, double step,
                                                        float norm_bw, const float* st, const float* out_base,
-                                                       size_t ostride, int* fail, const float2* rec, size_t rb) {
+                                                       size_t ostride, int* fail, const float2* rec, size_t rb,
+                                                       const double* side, size_t seg, int n_streams, bool major) {
     const int s = blockIdx.y;
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     const int nb = n / NB;
@@ -414,9 +415,36 @@ __global__ void __launch_bounds__(64) pll_check_kernel(const float* io, int n, s
     }
     const DeviceLib lib;
     bool same = true;
-    for (int j = 0; j < NB; j++) {
-        const float a = pll_step(p, ctx, x[j], Ki, Kp, step, lib);
-        same &= __float_as_uint(a) == __float_as_uint(o[j]);
+    bool done = false;
+    if (ctx.valid) {  // the batch on the certified fast path (~2.5x cheaper than 16 pll_step)
+        float v[NB], c[NB];
+        double iv[NB], pr[NB];
+        const double* siv = side;
+        const double* spr = side + seg * (size_t)n_streams;
+#pragma unroll
+        for (int j = 0; j < NB; j++) {
+            const size_t jj = (size_t)b * NB + j;
+            const size_t a = major ? (size_t)s * seg + jj : (jj / 2 * n_streams + s) * 2 + jj % 2;
+            v[j] = x[j];
+            iv[j] = siv[a];
+            pr[j] = spr[a];
+        }
+        const PllState p0 = p;
+        const PllCtx c0 = ctx;
+        if (pll_batch_fast<NB, false>(p, ctx, v, iv, pr, c, Ki, Kp, [](int) {})) {
+#pragma unroll
+            for (int j = 0; j < NB; j++) same &= __float_as_uint(c[j]) == __float_as_uint(o[j]);
+            done = true;
+        } else {
+            p = p0;
+            ctx = c0;
+        }
+    }
+    if (!done) {
+        for (int j = 0; j < NB; j++) {
+            const float a = pll_step(p, ctx, x[j], Ki, Kp, step, lib);
+            same &= __float_as_uint(a) == __float_as_uint(o[j]);
+        }
     }
     const float2 e = rec[(size_t)s * rb + b];
     same &= __float_as_uint(p.integ) == __float_as_uint(e.x) && __float_as_uint(p.phase) == __float_as_uint(e.y);
@@ -722,7 +750,7 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
             const int nb = m / kPllBatch;
             if (nb > 0)
                 hipLaunchKernelGGL(pll_check_kernel<kPllBatch>, dim3((nb + 63) / 64, n_streams), dim3(64), 0, s, x, m,
-                                   stride, step, norm_bw, st, args, seg, fail, rec, rb);
+                                   stride, step, norm_bw, st, args, seg, fail, rec, rb, side, seg, n_streams, spw <= 4);
         }
         if (spw <= 4)
             hipLaunchKernelGGL((pll_kernel<kPllBatch, true>), grid, block, 0, s, x, m, n_streams, spw, stride,
