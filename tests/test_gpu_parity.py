@@ -529,6 +529,17 @@ def test_rds_call_split_and_reset(fmrx, orc):
         assert same(rx.rds_block(demod)["rds"], z["rds"])
 
 
+@pytest.mark.parametrize("env", [{"FMRX_PLL_SPEC": "0"}, {"FMRX_PLL_SPEC_INJECT": "3"}])
+def test_rds_pll_speculation_fallbacks(fmrx, monkeypatch, env):
+    """The RDS loop (114 kHz, ncoScale 0.5) through the same speculative launch: the plain
+    certified launch and a runner with one corrupted batch both give the fixture's bits."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    z = load_rds("m0_rds57")
+    with fmrx.Receiver(0, fmrx.MONO) as rx:
+        assert same(rx.rds_block(z["demod"])["rds"], z["rds"])
+
+
 def test_rds_multistream_and_device_api(fmrx, orc):
     nif, nb = oracle.MODES[1][1], 10
     ins = [iqgen.make_rds_demod(60 + s, nb * nif, oracle.MODES[1][5]) for s in range(3)]
