@@ -363,10 +363,37 @@ FMRX_HD double split_w(double z, double z2, double z4, const SplitCoef& c) {
     const double Q = fma(z4, fma(z2, c.q[6], p45), fma(z2, p23, p01));
     return fma(z, Q, 1.0);
 }
+// Horner instead of Estrin: two multiplies fewer (z2, z4), a longer dependency chain -- for the
+// speculative runner, which is issue-bound, not latency-bound.  Same class of error.
+FMRX_HD double split_w_horner(double z, const SplitCoef& c) {
+    double Q = fma(z, c.q[6], c.q[5]);
+    Q = fma(z, Q, c.q[4]);
+    Q = fma(z, Q, c.q[3]);
+    Q = fma(z, Q, c.q[2]);
+    Q = fma(z, Q, c.q[1]);
+    Q = fma(z, Q, c.q[0]);
+    return fma(z, Q, 1.0);
+}
 // sin r, cos r in the split form: on the device lane_coef belongs to this lane (sin or cos by
 // lane parity) and the row broadcasts gather both; on the host both are evaluated.
+template <bool HORNER = false>
 FMRX_HD void pll_sincos_split(double r, const SplitCoef& lane_coef, double* sn, double* cs) {
-    const double z = r * r, z2 = z * z, z4 = z2 * z2;
+    const double z = r * r;
+    if constexpr (HORNER) {
+#ifdef __HIP_DEVICE_COMPILE__
+        const double w = split_w_horner(z, lane_coef);
+        const double rw = r * w;
+        const long long rw_bits = __builtin_bit_cast(long long, rw), w_bits = __builtin_bit_cast(long long, w);
+        *sn = __builtin_bit_cast(double, (long long)__builtin_amdgcn_mov_dpp(rw_bits, 0x150, 0xF, 0xF, false));
+        *cs = __builtin_bit_cast(double, (long long)__builtin_amdgcn_mov_dpp(w_bits, 0x151, 0xF, 0xF, false));
+#else
+        (void)lane_coef;
+        *sn = r * split_w_horner(z, split_coef(false));
+        *cs = split_w_horner(z, split_coef(true));
+#endif
+        return;
+    }
+    const double z2 = z * z, z4 = z2 * z2;
 #ifdef __HIP_DEVICE_COMPILE__
     const double w = split_w(z, z2, z4, lane_coef);
     const double rw = r * w;
@@ -467,7 +494,7 @@ FMRX_HD bool pll_batch_fast(PllState& p, PllCtx& ctx, const float (&v)[N], const
         const double r = fma(-nd, kPio2Lo, fma(-nd, kPio2Hi, x));
         if constexpr (!SPEC) acc_r = fmin(acc_r, fabs(r));
         if constexpr (SPLIT)
-            pll_sincos_split(r, sc, &sn, &cs);
+            pll_sincos_split<SPEC>(r, sc, &sn, &cs);
         else
             pll_sincos_kernel(r, &sn, &cs);
         fc = (float)cs;
