@@ -305,9 +305,10 @@ __global__ void __launch_bounds__(256) pll_kernel(float* io, int n, int n_stream
 // The certification inside pll_batch_fast is ~20 % of the serial step.  pll_spec_kernel runs
 // the recurrence WITHOUT it (pll_batch_fast<SPEC>): trigArg to out, and (integ, phase) at the
 // end of every batch to rec.  pll_check_kernel then recomputes every batch of every stream in
-// parallel, one thread each, with the exact pll_step from the state the runner recorded at
-// the end of the previous batch (batch 0: the true initial state st), and compares the 16
-// trigArgs and the end state bit for bit; fail[s] = the first batch that differs.  By
+// parallel, one thread each, exactly (the certified batch, pll_step where it cannot certify)
+// from the state the runner recorded at the end of the previous batch (batch 0: the true
+// initial state st), and compares the 16 trigArgs and the end state bit for bit; fail[s] =
+// the first batch that differs.  By
 // induction every batch before fail[s] is exact.  pll_kernel (with `fail`) resumes from there
 // on the certified path and runs the tail, so the result equals the plain launch bit for bit
 // whatever the runner did; when everything verified it only runs the tail.
@@ -385,7 +386,8 @@ __global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, i
     }
 }
 
-// One thread per (batch, stream): NB exact steps from the recorded start, compared bit for bit.
+// One thread per (batch, stream): NB exact steps from the recorded start, compared bit for
+// bit.  `major`: the side data's layout (stream-major for the split kernels, see launch_pll).
 template <int NB>
 __global__ void __launch_bounds__(64) pll_check_kernel(const float* io, int n, size_t stride, double step,
                                                        float norm_bw, const float* st, const float* out_base,
