@@ -1,8 +1,14 @@
-// cli.cpp — `fmrx [mode channels] [--batch N] [--device D] [--rf-taps T]`: the drop-in for the
-// reference's `project` executable (src/project.cpp:273-390).  Reads u8 I/Q from stdin, writes
-// raw S16LE to stdout: stereo = 2 channels interleaved R,L exactly like project.cpp:179-195;
-// mono = 1 channel (the private-history mono product; project.cpp logs `channels` but ignores
-// it).
+// cli.cpp — `fmrx [<mode> <channels>] [--batch N] [--device D] [--rf-taps T] [--mono-product]`:
+// the drop-in for the reference's `project` executable (src/project.cpp:273-390).  Reads u8 I/Q
+// from stdin and writes raw S16LE to stdout under project's process contract:
+//   * arguments as project.cpp:278-299: fewer than two positional arguments run the default
+//     mode 0 (a lone one is ignored, as `project 3` ignores it), exactly two are <mode>
+//     <channels> (atoi; out of range -> message, exit 1), more print the usage and exit 1;
+//   * the output is ALWAYS the 2-channel interleaved R,L stream of project.cpp:179-195:
+//     `channels` is only logged (:301-302), the reference has no mono-only output;
+//   * --mono-product (an fmrx extension, not a project argument) writes the 1-channel mono
+//     product instead (project.cpp:146's mono resample with a private history, quantised like
+//     :187) -- the BASELINE headline path.
 //
 // Streaming runtime.  The reference splits the work into a producer thread
 // (read + RF front end, project.cpp:48-84) and a consumer thread (audio back end, :132-196)
@@ -68,9 +74,10 @@ struct Slot {
 
 void usage(const char* argv0) {
     std::fprintf(stderr,
-                 "Usage: %s [<mode> <channels>] [--batch N] [--device D] [--rf-taps T]\n"
-                 "\t<mode> is a value from 0 to 3, <channels> is either 1 or 2\n",
-                 argv0);
+                 "Usage: %s\nor \nUsage %s <mode> <channels>\n"
+                 "\t\t<mode> is a value from 0 to 3\n\t\t   <channels> is either 1 or 2\n"
+                 "options (fmrx): [--batch N] [--device D] [--rf-taps T] [--mono-product]\n",
+                 argv0, argv0);
 }
 
 [[noreturn]] void die_hip(hipError_t e, const char* what) {
@@ -89,30 +96,36 @@ void usage(const char* argv0) {
 
 int main(int argc, char** argv) {
     int mode = 0, channels = 1, batch = 16, device = 0, rf_taps = 51;
+    bool mono_product = false;
     std::vector<const char*> pos;
     for (int i = 1; i < argc; i++) {
         if (!std::strcmp(argv[i], "--batch") && i + 1 < argc) batch = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--rf-taps") && i + 1 < argc) rf_taps = std::atoi(argv[++i]);
-        else if (argv[i][0] == '-') { usage(argv[0]); return 1; }
-        else pos.push_back(argv[i]);
+        else if (!std::strcmp(argv[i], "--mono-product")) mono_product = true;
+        else if (argv[i][0] == '-' && argv[i][1] != '\0' && !(argv[i][1] >= '0' && argv[i][1] <= '9')) {
+            usage(argv[0]);
+            return 1;
+        } else pos.push_back(argv[i]);  // "-1" is a (negative, invalid) mode as in project
     }
-    if (pos.size() == 2) {
+    if (pos.size() < 2) {  // project.cpp:278-279 (argc < 3): argv[1] alone is not parsed
+        std::fprintf(stderr, "Operating in default mode 0, mono\n");
+    } else if (pos.size() == 2) {  // :280-291
         mode = std::atoi(pos[0]);
         channels = std::atoi(pos[1]);
-    } else if (!pos.empty()) {
+        if (mode < 0 || mode > 3) { std::fprintf(stderr, "Invalid mode: %d!\n", mode); return 1; }
+        if (channels < 1 || channels > 2) { std::fprintf(stderr, "Invalid channel: %d!\n", channels); return 1; }
+    } else {  // :292-298
         usage(argv[0]);
         return 1;
-    } else {
-        std::fprintf(stderr, "Operating in default mode 0, mono\n");
     }
-    if (mode < 0 || mode > 3) { std::fprintf(stderr, "Invalid mode: %d!\n", mode); return 1; }
-    if (channels < 1 || channels > 2) { std::fprintf(stderr, "Invalid channel: %d!\n", channels); return 1; }
     if (batch < 1) batch = 1;
     std::fprintf(stderr, "Operating in mode %d, %s\n", mode, channels == 1 ? "mono" : "stereo");
 
+    // project.cpp always writes the stereo R,L stream whatever `channels` says (:179-195).
+    const int out_channels = mono_product ? FMRX_MONO : FMRX_STEREO;
     fmrx_config cfg;
-    if (fmrx_config_default(&cfg, mode, channels) != FMRX_OK) {
+    if (fmrx_config_default(&cfg, mode, out_channels) != FMRX_OK) {
         std::fprintf(stderr, "fmrx: %s\n", fmrx_last_error());
         return 1;
     }

@@ -466,21 +466,66 @@ def test_device_synth_equals_host(fmrx):
 
 # ---- the `project` drop-in CLI (stdin u8 -> stdout S16) --------------------------------------
 
-@pytest.mark.parametrize("mode,channels,batch", [(0, 2, 16), (0, 1, 3), (1, 2, 5), (2, 1, 1)])
-def test_cli_stdin_to_stdout(fmrx, orc, mode, channels, batch):
+def _cli(fmrx, args, data, timeout=300):
     import os
     import subprocess
 
-    bb, rf_fs = oracle.MODES[mode][0], oracle.MODES[mode][3]
-    nb = {0: 23, 1: 17, 2: 2}[mode]
-    iq = iqgen.make("synth:91", nb * bb + 4321, rf_fs)  # ragged tail is dropped
     exe = os.path.join(os.path.dirname(fmrx.LIB_PATH), "bin", "fmrx")
-    r = subprocess.run([exe, str(mode), str(channels), "--batch", str(batch)], input=iq.tobytes(),
-                       capture_output=True, timeout=300)
+    r = subprocess.run([exe] + [str(a) for a in args], input=data, capture_output=True, timeout=timeout)
+    return r
+
+
+# project.cpp:179-195 writes the 2-channel R,L stream whatever `channels` is (it is only logged,
+# :301-302), and fewer than two arguments select the default mode 0 (:278-279).
+@pytest.mark.parametrize("args,mode", [((), 0), (("3",), 0), ((0, 1), 0), ((0, 2), 0), ((1, 2), 1),
+                                       ((1, 1), 1), ((2, 1), 2), ((3, 2), 3)])
+@pytest.mark.parametrize("batch", [1, 5])
+def test_cli_project_contract(fmrx, orc, args, mode, batch):
+    bb, rf_fs = oracle.MODES[mode][0], oracle.MODES[mode][3]
+    nb = {0: 23, 1: 17, 2: 2, 3: 1}[mode]
+    if batch == 5 and mode >= 2:
+        pytest.skip("one batch covers the large-block modes")
+    iq = iqgen.make("synth:91", nb * bb + 4321, rf_fs)  # ragged tail is dropped
+    r = _cli(fmrx, list(args) + ["--batch", batch], iq.tobytes())
     assert r.returncode == 0, r.stderr.decode()
     got = np.frombuffer(r.stdout, np.int16)
-    want = orc.run(mode, 51, iq, ["pcm", "pcm_mono"])["pcm" if channels == 2 else "pcm_mono"]
+    want = orc.run(mode, 51, iq, ["pcm"])["pcm"]
+    assert got.size == nb * 2 * oracle.MODES[mode][2]
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("mode,rf_taps", [(0, 51), (0, 101), (2, 51)])
+def test_cli_mono_product_flag(fmrx, orc, mode, rf_taps):
+    bb, rf_fs = oracle.MODES[mode][0], oracle.MODES[mode][3]
+    nb = {0: 19, 2: 2}[mode]
+    iq = iqgen.make("synth:92", nb * bb, rf_fs)
+    r = _cli(fmrx, [mode, 1, "--mono-product", "--rf-taps", rf_taps, "--batch", 4], iq.tobytes())
+    assert r.returncode == 0, r.stderr.decode()
+    want = orc.run(mode, rf_taps, iq, ["pcm_mono"])["pcm_mono"]
+    assert np.array_equal(np.frombuffer(r.stdout, np.int16), want)
+
+
+def test_cli_bytes_equal_reference_project(fmrx, orc):
+    """Byte-compare `fmrx` and `fmrx 0 1` with the reference's own `project` executable
+    (oracle/_ref/project, built from src/project.cpp in place).  project exit(1)s at EOF while
+    blocks may still be queued (project.cpp:51-54), so its stdout is a prefix of the full
+    stream: compare on its length and require the full stream to equal the oracle's."""
+    import os
+    import subprocess
+
+    ref = os.path.join(os.path.dirname(os.path.dirname(fmrx.LIB_PATH)), "oracle", "_ref", "project")
+    if not os.path.exists(ref):
+        pytest.skip("oracle/_ref/project not built")
+    iq = iqgen.make("synth:93", 40 * 12800, 2400000).tobytes()
+    pr = subprocess.run([ref, "0", "1"], input=iq, capture_output=True, timeout=120)
+    want_prefix = pr.stdout
+    full = orc.run(0, 51, np.frombuffer(iq, np.uint8), ["pcm"])["pcm"].tobytes()
+    assert len(want_prefix) > 0 and full[: len(want_prefix)] == want_prefix
+    for args in ([], [0, 1]):
+        r = _cli(fmrx, args, iq)
+        assert r.returncode == 0, r.stderr.decode()
+        assert r.stdout == full
+        assert r.stdout[: len(want_prefix)] == want_prefix
 
 
 @pytest.mark.parametrize("nbytes", [0, 12799, 12800])

@@ -102,12 +102,14 @@ def test_synth_signal_is_fm_stereo(fmrx, orc):
 
 
 def test_cli_built_and_usage(fmrx):
+    """project.cpp:278-299's argument contract; every case exits before any GPU call."""
     exe = os.path.join(REPO, "software-defined-radio-course-project_amd", "bin", "fmrx")
     assert os.access(exe, os.X_OK)
-    r = subprocess.run([exe, "7", "1"], capture_output=True, timeout=60)
-    assert r.returncode == 1 and b"Invalid mode" in r.stderr
-    r = subprocess.run([exe, "0", "3"], capture_output=True, timeout=60)
-    assert r.returncode == 1 and b"Invalid channel" in r.stderr
+    for args, msg in ((["7", "1"], b"Invalid mode"), (["-1", "2"], b"Invalid mode"),
+                      (["0", "3"], b"Invalid channel"), (["0", "1", "2"], b"Usage"),
+                      (["--bogus"], b"Usage")):
+        r = subprocess.run([exe] + args, capture_output=True, timeout=60)
+        assert r.returncode == 1 and msg in r.stderr, (args, r.stderr)
 
 
 def test_build_flags_forbid_fma_and_fast_math():

@@ -49,8 +49,11 @@ def main():
     res = {"config": f"mode {args.mode}, {args.mib} MiB synthetic u8 I/Q on stdin -> S16 on stdout",
            "blocks": nbytes // bb, "batch_blocks": args.batch}
     outs = {}
+    # `fmrx <mode> 1` writes project's R,L stream like `<mode> 2` (project.cpp:179-195); the
+    # 1-channel mono product is the --mono-product extension
     runs = [("fmrx_stereo", [exe, str(args.mode), "2", "--batch", str(args.batch)]),
-            ("fmrx_mono", [exe, str(args.mode), "1", "--batch", str(args.batch)])]
+            ("fmrx_channels1", [exe, str(args.mode), "1", "--batch", str(args.batch)]),
+            ("fmrx_mono_product", [exe, str(args.mode), "1", "--mono-product", "--batch", str(args.batch)])]
     ref = os.path.join(REPO, "oracle", "_ref", "project")
     if not args.no_reference and os.path.exists(ref):
         runs.append(("reference_project", [ref, str(args.mode), "2"]))
@@ -70,6 +73,7 @@ def main():
         a, b = outs["reference_project"], outs["fmrx_stereo"]
         res["reference_prefix_bit_exact"] = bool(len(a) <= len(b) and np.array_equal(a, b[: len(a)]))
         res["reference_blocks_written"] = int(len(a) // (2 * oracle.MODES[args.mode][2]))
+    res["channels1_equals_stereo"] = bool(np.array_equal(outs["fmrx_channels1"], outs["fmrx_stereo"]))
     for f in os.listdir(tmp):
         os.remove(os.path.join(tmp, f))
     os.rmdir(tmp)
