@@ -180,6 +180,15 @@ int fmrx_synth_host(uint64_t seed, int rf_fs, uint64_t first_pair, size_t n_pair
 int fmrx_synth_device(fmrx_ctx* ctx, uint64_t seed, int rf_fs, uint64_t first_pair,
                       size_t n_pairs, uint8_t* d_out);
 
+/* ---- test hook: the PLL's fallback libm (src/filter.cpp:161,168-170 on refused args) ---- */
+/* Runs the device functions the PLL calls where its certified fast paths refuse, on device
+ * buffers (context stream, async): kind 0 -> d_out[2i] = float(sin a_i), d_out[2i+1] =
+ * float(cos a_i); kind 1 -> d_out[i] = float(atan2(a_i, b_i)); kind 2 -> d_out[i] = the NCO's
+ * float(cos a_i).  tests/test_gpu_parity.py checks them against glibc's floats
+ * (tests/golden/pll_fallback.npz).                                                         */
+int fmrx_test_pll_fallback(fmrx_ctx* ctx, int kind, const float* d_a, const float* d_b, size_t n,
+                           float* d_out);
+
 #ifdef __cplusplus
 }
 #endif

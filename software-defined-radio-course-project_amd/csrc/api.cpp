@@ -933,6 +933,15 @@ int fmrx_quantize(fmrx_ctx* c, const float* d_x, size_t n, int16_t* d_out) {
     return launch_quantize(d_x, n, d_out, c->stream) ? fail(FMRX_EHIP, "launch failed") : 0;
 }
 
+int fmrx_test_pll_fallback(fmrx_ctx* c, int kind, const float* d_a, const float* d_b, size_t n, float* d_out) {
+    CtxLock lock_(c);
+    if (!c || kind < 0 || kind > 2 || (n && (!d_a || !d_out || (kind == 1 && !d_b))))
+        return fail(FMRX_EINVAL, "bad argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return launch_pll_fallback_test(kind, d_a, d_b, n, d_out, c->stream) ? fail(FMRX_EHIP, "launch failed") : 0;
+}
+
 // ---- synthetic input --------------------------------------------------------------------
 int fmrx_synth_host(uint64_t seed, int rf_fs, uint64_t first_pair, size_t n_pairs, uint8_t* out) {
     if (!out || rf_fs <= 0) return fail(FMRX_EINVAL, "bad argument");

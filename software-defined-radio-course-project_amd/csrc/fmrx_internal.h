@@ -87,6 +87,9 @@ size_t pll_side_doubles(int n, int n_streams);
 int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
                float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s);
 
+// test hook: the PLL's fallback libm on device (kind 0 sincos, 1 atan2, 2 NCO cos)
+int launch_pll_fallback_test(int kind, const float* a, const float* b, size_t n, float* out, hipStream_t s);
+
 struct AudioLaunch {
     const float* demod;     // with hist samples in front (per stream stride demod_stride)
     size_t demod_stride;

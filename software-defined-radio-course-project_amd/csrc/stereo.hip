@@ -15,6 +15,7 @@
 
 #include "dsp_device.h"
 #include "fmrx_internal.h"
+#include "pll_cr.h"
 #include "pll_math.h"
 
 namespace fmrx {
@@ -72,15 +73,23 @@ __global__ void bpf_pair_generic(StereoLaunch L, BpTaps t) {
 // The recurrence only needs atan2 and sincos; the NCO output cos(trigArg * ncoScale +
 // phaseAdjust) (filter.cpp:170) depends on nothing later, so the serial loop stores trigArg
 // in place and pll_nco_kernel evaluates the NCO for all samples in parallel afterwards.
-// Full-precision fallbacks (HIP's double atan2/sin/cos), out of line: taken ~1e-6 of steps.
+// Fallbacks where a certified fast path refuses (~1e-6 of steps), out of line: pll_cr.h's
+// double-double evaluation rounded like glibc (float of the correctly rounded double), pinned to
+// glibc on every refusable sincos argument of the PLL's domain (tools/check_pll_cr.cpp,
+// tests/golden/pll_fallback.npz).  HIP's double sin/cos only beyond |x| >= 2^31, a trigArg no
+// PLL state reaches (|trigArg| < 1e9 wherever the step's product is finite).
 __device__ __noinline__ float atan2_lib(float y, float x) {
     float e;
     if (fast_atan2_f(y, x, &e)) return e;
-    return static_cast<float>(atan2(static_cast<double>(y), static_cast<double>(x)));
+    return cr::atan2_f(y, x);
 }
 __device__ __noinline__ float2 sincos_lib(float a) {
-    return make_float2(static_cast<float>(sin(static_cast<double>(a))),
-                       static_cast<float>(cos(static_cast<double>(a))));
+    if (!cr::sincos_domain(a))
+        return make_float2(static_cast<float>(sin(static_cast<double>(a))),
+                           static_cast<float>(cos(static_cast<double>(a))));
+    float sv, cv;
+    cr::sincos_f(a, &sv, &cv);
+    return make_float2(sv, cv);
 }
 
 struct DeviceLib {
@@ -463,9 +472,28 @@ __global__ void pll_nco_kernel(float* io, int n, size_t stride, const float* arg
     float* x = io + (size_t)s * stride;
     const float a = args[(size_t)s * astride + i] * nco_scale + phase_adjust;
     float sv, cv;
-    if (!fast_sincos_f(a, &sv, &cv)) cv = static_cast<float>(cos(static_cast<double>(a)));
+    if (!fast_sincos_f(a, &sv, &cv)) cv = sincos_lib(a).y;
     x[i] = cv;
     if (i == n - 1) st[8 * (size_t)s + 4] = cv;
+}
+
+// Test hook (fmrx_test_pll_fallback): the PLL's out-of-line fallbacks on given arguments.
+// kind 0: sincos_lib(a) -> out[2i] = sin, out[2i + 1] = cos; kind 1: atan2_lib(a = y, b = x);
+// kind 2: the NCO's cos (pll_nco_kernel: fast_sincos_f, else the fallback).
+__global__ void pll_fallback_test_kernel(int kind, const float* a, const float* b, size_t n, float* out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (kind == 0) {
+        const float2 r = sincos_lib(a[i]);
+        out[2 * i] = r.x;
+        out[2 * i + 1] = r.y;
+    } else if (kind == 1) {
+        out[i] = atan2_lib(a[i], b[i]);
+    } else {
+        float sv, cv;
+        if (!fast_sincos_f(a[i], &sv, &cv)) cv = sincos_lib(a[i]).y;
+        out[i] = cv;
+    }
 }
 
 // ---- audio stage -------------------------------------------------------------------------
@@ -778,6 +806,13 @@ int launch_stereo_audio(const AudioLaunch& L, int n_streams, hipStream_t s) {
     }
     hipLaunchKernelGGL(stereo_state_kernel, dim3(n_streams), dim3(kTail), 0, s, L);
     return ok();
+}
+
+int launch_pll_fallback_test(int kind, const float* a, const float* b, size_t n, float* out, hipStream_t s) {
+    if (n == 0) return 0;
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(pll_fallback_test_kernel, dim3(grid), dim3(256), 0, s, kind, a, b, n, out);
+    return hipGetLastError() != hipSuccess;
 }
 
 }  // namespace fmrx

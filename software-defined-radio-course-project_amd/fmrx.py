@@ -82,6 +82,7 @@ PROTOTYPES = {
     "fmrx_quantize": (C.c_int, [_vp, _vp, _sz, _vp]),
     "fmrx_synth_host": (C.c_int, [C.c_uint64, C.c_int, C.c_uint64, _sz, _vp]),
     "fmrx_synth_device": (C.c_int, [_vp, C.c_uint64, C.c_int, C.c_uint64, _sz, _vp]),
+    "fmrx_test_pll_fallback": (C.c_int, [_vp, C.c_int, _vp, _vp, _sz, _vp]),
 }
 
 _lib = None
@@ -337,6 +338,10 @@ class Receiver:
 
     def quantize(self, d_x, n, d_out) -> None:
         _check(lib().fmrx_quantize(self.h, d_x, n, d_out))
+
+    def test_pll_fallback(self, kind: int, d_a, d_b, n: int, d_out) -> None:
+        """Test hook: the PLL's fallback libm on device (0 sincos, 1 atan2, 2 NCO cos)."""
+        _check(lib().fmrx_test_pll_fallback(self.h, kind, d_a, d_b, n, d_out))
 
 
 def build() -> None:

@@ -464,6 +464,35 @@ def test_device_synth_equals_host(fmrx):
         assert np.array_equal(d.cpu().numpy(), fmrx.synth_host(9, 2400000, 123456, 300001))
 
 
+# ---- the PLL's fallback libm (refused arguments) against glibc ---------------------------------
+
+def test_pll_fallback_matches_glibc(fmrx):
+    """Where the PLL's certified fast paths refuse, the device falls back to csrc/pll_cr.h; its
+    floats must equal glibc's (filter.cpp:161,168-170) on every refusable argument of the fixture
+    (all hard sin/cos arguments |x| < 1e9 and a sample beyond, hard atan2 pairs)."""
+    import os
+
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "pll_fallback.npz"))
+    with fmrx.Receiver(0, fmrx.STEREO) as rx:
+        x = torch.from_numpy(z["sincos_x"]).cuda()
+        out = torch.empty(2 * x.numel(), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        rx.test_pll_fallback(0, x.data_ptr(), None, x.numel(), out.data_ptr())
+        rx.synchronize()
+        got = out.cpu().numpy().reshape(-1, 2)
+        assert same(got[:, 0], z["sincos_s"]) and same(got[:, 1], z["sincos_c"])
+        nco = torch.empty(x.numel(), dtype=torch.float32, device="cuda")
+        rx.test_pll_fallback(2, x.data_ptr(), None, x.numel(), nco.data_ptr())
+        rx.synchronize()
+        assert same(nco.cpu().numpy(), z["sincos_c"])
+        y, xx = torch.from_numpy(z["atan2_y"]).cuda(), torch.from_numpy(z["atan2_x"]).cuda()
+        e = torch.empty(y.numel(), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        rx.test_pll_fallback(1, y.data_ptr(), xx.data_ptr(), y.numel(), e.data_ptr())
+        rx.synchronize()
+        assert same(e.cpu().numpy(), z["atan2_e"])
+
+
 # ---- the `project` drop-in CLI (stdin u8 -> stdout S16) --------------------------------------
 
 def _cli(fmrx, args, data, timeout=300):

@@ -75,3 +75,41 @@ def test_pll_recurrence_bit_exact(runner, orc, tmp_path, recipe, seconds, chunk,
     batches, redone = (int(t.split("=")[1]) for t in r.stdout.split("\n")[-3].split())
     if recipe.startswith("synth"):
         assert redone <= 0.05 * batches, r.stdout
+
+
+@pytest.fixture(scope="module")
+def cr_checker(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("pllcr") / "check_pll_cr")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-pthread", "-o", exe,
+                    os.path.join(REPO, "tools", "check_pll_cr.cpp")], check=True)
+    return exe
+
+
+def test_fallback_sincos_equals_glibc_on_every_refusable_argument(cr_checker, tmp_path):
+    """The device's sin/cos fallback (csrc/pll_cr.h: double-double, rounded like a correctly
+    rounded double libm) against glibc on EVERY float |x| in [2^-19, 2^30) any fast path can
+    refuse (filter.cpp:168-170's float(glibc sin/cos)), plus every 997th other float."""
+    r = subprocess.run([cr_checker, "sincos", str(tmp_path / "sc.bin")], capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0 and "mismatches=0" in r.stdout, r.stdout
+
+
+def test_fallback_atan2_equals_glibc_on_refusable_pairs(cr_checker, tmp_path):
+    r = subprocess.run([cr_checker, "atan2", "200000000", "11", str(tmp_path / "at.bin")], capture_output=True,
+                       text=True, timeout=900)
+    assert r.returncode == 0 and "mismatches=0" in r.stdout, r.stdout
+
+
+def test_fallback_fixture_provenance():
+    import numpy as np
+
+    z = np.load(os.path.join(REPO, "tests", "golden", "pll_fallback.npz"))
+    assert "mismatches=0" in str(z["sweep_sincos"]) and "mismatches=0" in str(z["sweep_atan2"])
+    assert len(z["sincos_x"]) > 1000 and len(z["atan2_y"]) > 1000
+    # the fixture's values are glibc's: spot-check against this host's libm where it is 2.35
+    if os.confstr("CS_GNU_LIBC_VERSION") == str(z["glibc"]):
+        import math
+
+        x = [float(v) for v in z["sincos_x"][::97]]
+        assert np.array_equal(np.array([math.sin(v) for v in x], np.float32), z["sincos_s"][::97])
+        assert np.array_equal(np.array([math.cos(v) for v in x], np.float32), z["sincos_c"][::97])

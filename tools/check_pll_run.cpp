@@ -1,7 +1,7 @@
 // tools/check_pll_run.cpp — run the whole PLL recurrence (src/filter.cpp:136-174) two ways on
 // the host and require bit-identical output: (a) the reference's arithmetic with glibc's
-// double atan2/cos/sin, (b) csrc/pll_math.h's pll_step (certified fast paths + glibc
-// fallbacks), (c) pll_kernel's schedule: side data per chunk (pll_side, as pll_prep_kernel),
+// double atan2/cos/sin, (b) csrc/pll_math.h's pll_step (certified fast paths + the device's
+// pll_cr.h fallbacks), (c) pll_kernel's schedule: side data per chunk (pll_side, as pll_prep_kernel),
 // 16-sample pll_batch_fast batches, a batch redone with pll_step when it cannot be certified,
 // the tail with pll_step -- the GPU's arithmetic.
 // Usage: check_pll_run <carrier.f32> <freq> <fs> [chunk] [split=1]   (state carried across chunks)
@@ -12,17 +12,24 @@
 #include <cstring>
 #include <vector>
 
+#include "../software-defined-radio-course-project_amd/csrc/pll_cr.h"
 #include "../software-defined-radio-course-project_amd/csrc/pll_math.h"
 
+// the fallbacks exactly as the device's DeviceLib (csrc/stereo.hip): fdlibm atan2, then the
+// double-double pll_cr.h evaluations; glibc only beyond the cr domain (as the device's ocml)
 struct GlibcLib {
     float atan2f_(float y, float x) const {
         float e;
         if (fmrx::fast_atan2_f(y, x, &e)) return e;
-        return (float)std::atan2((double)y, (double)x);
+        return fmrx::cr::atan2_f(y, x);
     }
     void sincosf_(float a, float* s, float* c) const {
-        *s = (float)std::sin((double)a);
-        *c = (float)std::cos((double)a);
+        if (!fmrx::cr::sincos_domain(a)) {
+            *s = (float)std::sin((double)a);
+            *c = (float)std::cos((double)a);
+            return;
+        }
+        fmrx::cr::sincos_f(a, s, c);
     }
 };
 
