@@ -45,6 +45,59 @@ def kernel_name() -> str:
     return _VARIANTS[int(os.environ.get("FMRX_MONO_VARIANT", "6"))]  # csrc kDefaultVariant
 
 
+KERNEL_SOURCES = ("mono_fused.hip", "dsp_device.h", "fmrx_internal.h")
+
+
+def kernel_source_hash() -> str:
+    """sha256 over the fused kernel's sources: profiles/traffic_mono101.json carries the hash of
+    the sources its PMC passes ran, and bench.py reports `traffic` only while they still match."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(REPO, "software-defined-radio-course-project_amd", "csrc", f), "rb") as g:
+            h.update(g.read())
+    return h.hexdigest()[:16]
+
+
+def host_info() -> dict:
+    """The host the CPU baselines run on (SURVEY §8d ii): CPU model, nproc, the affinity mask,
+    a cgroup CPU quota if any, and the cores the baseline may use.  On the gpurun box nproc and
+    the affinity mask show the whole machine; the box's CPU share is exported as
+    OMP_NUM_THREADS (16 per GPU), which the all-cores baseline honours."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+            if path.endswith("cpu.max") and parts[0] != "max":
+                quota = int(parts[0]) / int(parts[1])
+            elif path.endswith("quota_us") and int(parts[0]) > 0:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as g:
+                    quota = int(parts[0]) / int(g.read())
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    usable = affinity
+    if quota is not None:
+        usable = min(usable, max(1, int(quota)))
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        usable = min(usable, int(share))
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "cpu_share_env": share, "usable_cores": usable}
+
+
 def flops_per_iq(rf_taps: int) -> float:
     # per IQ pair (SURVEY §8a): RF 2 ch x taps x (mul+add) / 10, demod ~9/10, audio 51x2/50
     return 2 * rf_taps * 2 / 10 + 0.9 + 51 * 2 / 50
@@ -126,6 +179,7 @@ def main() -> None:
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     flops = flops_per_iq(RF_TAPS) * n_iq
     line = {
+        # value = whole-job aggregate over all ranks (per_gpu_MS_s = value / n_gpus)
         "metric": "IQ Msamples/s (and x real-time) per GPU, mode-0 mono 2.4MS/s->48kS/s",
         "value": round(value, 1),
         "unit": "MS/s",
@@ -167,14 +221,32 @@ def main() -> None:
             "flop_per_iq": round(flops_per_iq(RF_TAPS), 2),
         },
     }
+    # binding roof: the kernel is bound by the FP32 VALU without FMA (bit parity), not by HBM
+    line["roofline"]["binding"] = dict(line["compute"])
+    # PMC traffic of record, only while it was measured on this kernel's sources
     traffic_file = os.path.join(REPO, "profiles", "traffic_mono101.json")
     if os.path.exists(traffic_file):
         with open(traffic_file) as f:
-            line["roofline"]["traffic"] = json.load(f).get("hbm_bytes_per_launch")
+            rec = json.load(f)
+        if rec.get("kernel") == kernel_name() and rec.get("kernel_source_sha256") == kernel_source_hash():
+            line["roofline"]["traffic"] = rec.get("hbm_bytes_per_launch")
+            line["roofline"]["traffic_source"] = rec.get("source")
+            if rec.get("effective_clock_ghz"):
+                line["roofline"]["binding"]["effective_clock_ghz_pmc"] = rec["effective_clock_ghz"]
+                line["roofline"]["binding"]["frac_at_effective_clock"] = round(
+                    line["compute"]["frac"] * 2.4 / rec["effective_clock_ghz"], 4)
+        else:
+            line["roofline"]["traffic_note"] = "profiles/traffic_mono101.json is for other kernel sources: not reported"
+    line["per_gpu_MS_s"] = round(value / world, 1)
+    line["aggregate_MS_s"] = round(value, 1)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the contract: rank 0 at N=1 only
+        host = host_info()
         line["cpu_baseline"] = cpu_baseline(d_iq, d_pcm, args.cpu_sample_bytes, bb, na)
-        line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(d_iq, args.cpu_sample_bytes, bb)
+        line["cpu_baseline"]["host"] = host
+        line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(d_iq, args.cpu_sample_bytes, bb, host["usable_cores"])
+        if line["cpu_baseline_all_cores"] is not None:
+            line["cpu_baseline_all_cores"]["host"] = host
     if world == 1 and not args.no_other_configs:
         del d_iq, d_pcm
         torch.cuda.empty_cache()
@@ -199,7 +271,9 @@ def other_configs(fmrx) -> dict:
         iq = torch.empty(nb * bb, dtype=torch.uint8, device="cuda")
         pcm = torch.empty(nb * rx.geo.pcm_samples, dtype=torch.int16, device="cuda")
         rx.synth_device(3000, 0, nb * bb // 2, iq.data_ptr())
-        rx.process_device(iq.data_ptr(), 16, pcm.data_ptr())  # warm-up, then from the start
+        # warm-up at full size (the first full-size call grows the demod / band-pass / PLL
+        # scratch buffers; that allocation must not sit inside the timed call), then restart
+        rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
         rx.synchronize()
         rx.reset()
         t0 = time.perf_counter()
@@ -286,7 +360,7 @@ def _ref_worker(args):
     return t0, time.perf_counter()
 
 
-def cpu_baseline_all_cores(d_iq, sample_bytes, bb):
+def cpu_baseline_all_cores(d_iq, sample_bytes, bb, cores):
     """the reference's mono path with one stream per host core, all at once.
     The GiB is cut into one contiguous slice per core (each slice an independent stream, so
     only the timing is meaningful); spawned processes, no GPU.  Rate = bytes / wall span."""
@@ -297,7 +371,7 @@ def cpu_baseline_all_cores(d_iq, sample_bytes, bb):
 
     if not oracle.reference_available():
         return None
-    cores = max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")), 16))
+    cores = max(1, cores)  # host_info()["usable_cores"]
     nbs = sample_bytes // bb
     host = d_iq[: nbs * bb].cpu().numpy()
     per = nbs // cores

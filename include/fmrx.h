@@ -56,7 +56,13 @@ typedef struct {
     int rf_taps;     /* RF LPF taps, reference 51 (project.cpp:306); 0 = default              */
     int bp_taps;     /* stereo band-pass taps, reference 51 (project.cpp:307); 0 = default   */
     int audio_taps;  /* audio LPF taps per phase: 51 only (project.cpp:319; x up in 2/3)    */
-    int n_streams;   /* independent IQ streams processed per call (>=1)                        */
+    int n_streams;   /* independent IQ streams processed per call (>=1, <= the device's grid.y */
+                     /* limit; fmrx_create refuses more with FMRX_EINVAL).  Device memory per   */
+                     /* stream: 2 halos (~26 KiB) + the audio history; stereo adds the demod /  */
+                     /* channel / carrier rows (3 x 4 B per IF sample of a call) and the PLL    */
+                     /* scratch, ~32.5 B per sample of a segment (2^18 samples per stream, fewer */
+                     /* past 32 streams: segment x streams ~2^23, >= 2^14 -- ~0.5 MB a stream at */
+                     /* 2,048 streams).                                                           */
     int device;      /* HIP device ordinal                                                     */
 } fmrx_config;
 
@@ -188,6 +194,14 @@ int fmrx_synth_device(fmrx_ctx* ctx, uint64_t seed, int rf_fs, uint64_t first_pa
  * (tests/golden/pll_fallback.npz).                                                         */
 int fmrx_test_pll_fallback(fmrx_ctx* ctx, int kind, const float* d_a, const float* d_b, size_t n,
                            float* d_out);
+
+/* ---- diagnostic: clock stamps of the fused mono kernel ---------------------------------- */
+/* With d_stamps set, the mode-0 101-tap fused kernel (default variant) also writes, per     *
+ * workgroup w, 6 u64 at d_stamps[6w..]: shader-clock counter at start and end, the 100 MHz  *
+ * counter at start and end, HW_ID, XCC_ID (tools/mono_stamps.py: effective clock, wave       *
+ * lifetimes, per-XCD balance).  Results are unchanged.  *needed = the largest grid a call    *
+ * can launch (n_streams x 256 x resident workgroups per CU).  d_stamps = NULL turns it off. */
+int fmrx_debug_mono_stamps(fmrx_ctx* ctx, unsigned long long* d_stamps, size_t n_workgroups, size_t* needed);
 
 #ifdef __cplusplus
 }

@@ -44,7 +44,8 @@ int fail(int code, const char* fmt, ...) {
 constexpr int kDemodHist = 64;   // demod samples kept in front of each call (>= bp_taps-1)
 constexpr int kMixTail = 64;     // must match stereo.hip kTail
 constexpr uint32_t kStateMagic = 0x46524D58u;  // "FMRX"
-constexpr uint32_t kStateVersion = 1;
+constexpr uint32_t kStateVersion = 2;  // 2: + flags word (bit 0: audio history stale after fmrx_seek)
+constexpr int kStateHdrWords = 10;  // magic, version, mode, channels, rf_taps, n_streams, halo, audio_hist, flags, 0
 
 template <class T>
 struct DevBuf {
@@ -116,6 +117,7 @@ struct fmrx_ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
     size_t ev_used = 0;
     bool timing = false;
+    unsigned long long* stamps = nullptr;  // fmrx_debug_mono_stamps (diagnostic)
 };
 
 namespace {
@@ -264,6 +266,7 @@ int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
     L.halo_bytes = c->halo_bytes;
     L.n_if = (long long)(n_blocks * c->geo.if_samples);
     L.segs = mono_segments(c, L.n_if);
+    L.stamps = c->stamps;
     L.audio = with_audio ? 1 : 0;
     const int ad = c->geo.audio_up == 1 ? c->geo.audio_down : 5;
     std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
@@ -296,18 +299,27 @@ int run_mono_audio(fmrx_ctx* c, const float* d_demod, size_t demod_stride, size_
     const int ns = c->cfg.n_streams;
     const int at = c->geo.audio_taps_total;
     const size_t na = n_if * c->geo.audio_up / c->geo.audio_down;
-    int rc = c->d_scratch.ensure(na * ns);
-    if (rc) return rc;
-    for (int s = 0; s < ns; s++) {
-        const float* in = d_demod + s * demod_stride;
-        float* st = c->d_audio_hist.p + (size_t)s * c->audio_hist;
-        float* out = d_mono ? d_mono + s * na : c->d_scratch.p + s * na;
-        rc = launch_polyphase(out, st, in, c->d_audio.p, at, c->geo.audio_up, c->geo.audio_down, (int)na,
-                              c->stream);
-        if (rc == 0) rc = launch_tail_copy(st, in + (n_if - (at - 1)), at - 1, c->stream);
-        if (rc == 0) rc = launch_quantize(out, na, d_pcm + s * na, c->stream);
-        if (rc) return fail(FMRX_EHIP, "mono audio stage launch failed");
-    }
+    // every stream in one launch: the resampler (+ the quantiser) over (output, stream), then
+    // the history move of every stream (after all reads of the old history)
+    PolyStreams P{};
+    P.in = d_demod;
+    P.in_stride = demod_stride;
+    P.state = c->d_audio_hist.p;
+    P.state_stride = c->audio_hist;
+    P.coeff = c->d_audio.p;
+    P.taps = at;
+    P.up = c->geo.audio_up;
+    P.down = c->geo.audio_down;
+    P.n_out = (int)na;
+    P.out = d_mono;
+    P.out_stride = na;
+    P.pcm = d_pcm;
+    P.pcm_stride = na;
+    int rc = launch_polyphase(P, ns, c->stream);
+    if (rc == 0 && n_if >= (size_t)(at - 1))
+        rc = launch_copy_streams(c->d_audio_hist.p, c->audio_hist, d_demod + (n_if - (at - 1)), demod_stride,
+                                 at - 1, ns, c->stream);
+    if (rc) return fail(FMRX_EHIP, "mono audio stage launch failed");
     return 0;
 }
 
@@ -352,12 +364,11 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
     A.at = c->geo.audio_taps_total;
     A.audio_c = c->d_audio.p;
     if (launch_stereo_audio(A, ns, c->stream)) return fail(FMRX_EHIP, "stereo audio launch failed");
-    // demod history for the next call: last kDemodHist samples -> front
-    for (int s = 0; s < ns; s++) {
-        float* base = c->d_demod.p + (size_t)s * c->demod_stride;
-        if (launch_tail_copy(base, base + n_if, kDemodHist, c->stream))
-            return fail(FMRX_EHIP, "demod history copy failed");
-    }
+    // demod history for the next call: last kDemodHist samples -> front, every stream in one
+    // launch (n_if >= one block of IF samples > kDemodHist: the ranges never overlap)
+    if (launch_copy_streams(c->d_demod.p, c->demod_stride, c->d_demod.p + n_if, c->demod_stride, kDemodHist, ns,
+                            c->stream))
+        return fail(FMRX_EHIP, "demod history copy failed");
     return 0;
 }
 
@@ -448,6 +459,13 @@ int fmrx_create(const fmrx_config* cfg, fmrx_ctx** out) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return fail(FMRX_EHIP, "no HIP device available (libfmrx has no CPU path)");
     if (cfg->device < 0 || cfg->device >= ndev) return fail(FMRX_EINVAL, "bad device %d", cfg->device);
+    // every per-stream launch puts the streams on grid.y (band-pass, PLL check / NCO / pre-pass,
+    // halo update, the multi-stream audio and copy kernels): refuse what cannot launch here
+    // rather than fail at the first call
+    int max_y = 0;
+    if (hipDeviceGetAttribute(&max_y, hipDeviceAttributeMaxGridDimY, cfg->device) == hipSuccess && max_y > 0 &&
+        cfg->n_streams > max_y)
+        return fail(FMRX_EINVAL, "n_streams %d exceeds the device's grid.y limit %d", cfg->n_streams, max_y);
     fmrx_ctx* c = new fmrx_ctx();
     c->cfg = *cfg;
     c->cfg.rf_taps = g.rf_taps;
@@ -572,7 +590,7 @@ int fmrx_state_size(const fmrx_ctx* c, size_t* bytes) {
     CtxLock lock_(c);
     if (!c || !bytes) return fail(FMRX_EINVAL, "null argument");
     const size_t ns = c->cfg.n_streams;
-    *bytes = 8 * sizeof(uint32_t) + ns * (c->halo_bytes + sizeof(float) * (c->audio_hist + kDemodHist + 8 + kMixTail + 8));
+    *bytes = kStateHdrWords * sizeof(uint32_t) + ns * (c->halo_bytes + sizeof(float) * (c->audio_hist + kDemodHist + 8 + kMixTail + 8));
     return FMRX_OK;
 }
 
@@ -595,11 +613,18 @@ int state_io(fmrx_ctx* c, uint8_t* buf, size_t bytes, bool put) {
     if (bytes < need) return fail(FMRX_ESTATE, "state buffer too small (%zu < %zu)", bytes, need);
     int rc = set_device(c);
     if (rc) return rc;
-    uint32_t hdr[8] = {kStateMagic, kStateVersion, (uint32_t)c->cfg.mode, (uint32_t)c->cfg.channels,
-                       (uint32_t)c->geo.rf_taps, (uint32_t)c->cfg.n_streams, (uint32_t)c->halo_bytes,
-                       (uint32_t)c->audio_hist};
+    // words 0-7 identify the context shape and must match; word 8 carries the audio-history
+    // staleness of a context taken between fmrx_seek and its next fused call (restored with
+    // the blob, so fmrx_audio_block refuses the stale history there too)
+    uint32_t hdr[kStateHdrWords] = {kStateMagic, kStateVersion, (uint32_t)c->cfg.mode, (uint32_t)c->cfg.channels,
+                                    (uint32_t)c->geo.rf_taps, (uint32_t)c->cfg.n_streams, (uint32_t)c->halo_bytes,
+                                    (uint32_t)c->audio_hist, c->audio_hist_stale ? 1u : 0u, 0u};
     if (put) {
-        if (std::memcmp(hdr, buf, sizeof hdr) != 0) return fail(FMRX_ESTATE, "state blob does not match this context");
+        if (std::memcmp(hdr, buf, 8 * sizeof(uint32_t)) != 0)
+            return fail(FMRX_ESTATE, "state blob does not match this context");
+        uint32_t flags;
+        std::memcpy(&flags, buf + 8 * sizeof(uint32_t), sizeof flags);
+        if (flags > 1u) return fail(FMRX_ESTATE, "state blob: unknown flags 0x%x", flags);
     } else {
         std::memcpy(buf, hdr, sizeof hdr);
     }
@@ -609,8 +634,13 @@ int state_io(fmrx_ctx* c, uint8_t* buf, size_t bytes, bool put) {
     BlobIO b{buf + sizeof hdr, put};
     if ((rc = b.io(c, c->d_halo[c->halo_cur].p, ns * c->halo_bytes))) return rc;
     if ((rc = b.io(c, c->d_audio_hist.p, ns * sizeof(float) * c->audio_hist))) return rc;
-    for (size_t s = 0; s < ns; s++)
-        if ((rc = b.io(c, c->d_demod.p + s * c->demod_stride, sizeof(float) * kDemodHist))) return rc;
+    // demod history: kDemodHist floats in front of each stream's row (one 2-D copy)
+    {
+        const size_t w = sizeof(float) * kDemodHist, pitch = sizeof(float) * c->demod_stride;
+        if (put) HIPCHK(hipMemcpy2DAsync(c->d_demod.p, pitch, b.p, w, w, ns, hipMemcpyHostToDevice, c->stream));
+        else HIPCHK(hipMemcpy2DAsync(b.p, w, c->d_demod.p, pitch, w, ns, hipMemcpyDeviceToHost, c->stream));
+        b.p += w * ns;
+    }
     if ((rc = b.io(c, c->d_pll.p, ns * sizeof(float) * 8))) return rc;
     if ((rc = b.io(c, c->d_mix_tail.p, ns * sizeof(float) * kMixTail))) return rc;
     if ((rc = b.io(c, c->d_mono_state.p, ns * sizeof(float) * 8))) return rc;
@@ -628,8 +658,13 @@ int fmrx_get_state(fmrx_ctx* c, void* buf, size_t bytes) {
 int fmrx_set_state(fmrx_ctx* c, const void* buf, size_t bytes) {
     CtxLock lock_(c);
     if (!c || !buf) return fail(FMRX_EINVAL, "null argument");
-    const int rc = state_io(c, static_cast<uint8_t*>(const_cast<void*>(buf)), bytes, true);
-    if (rc == 0) c->audio_hist_stale = false;
+    const uint8_t* p = static_cast<const uint8_t*>(buf);
+    const int rc = state_io(c, const_cast<uint8_t*>(p), bytes, true);
+    if (rc == 0) {
+        uint32_t flags;
+        std::memcpy(&flags, p + 8 * sizeof(uint32_t), sizeof flags);
+        c->audio_hist_stale = (flags & 1u) != 0;
+    }
     return rc;
 }
 
@@ -966,3 +1001,15 @@ int fmrx_synth_device(fmrx_ctx* c, uint64_t seed, int rf_fs, uint64_t first_pair
 }
 
 }  // extern "C"
+
+// Diagnostic: per-workgroup clock stamps of the fused mono kernel (default variant, mode 0,
+// 101-tap RF); the kernel's results are unchanged.  d_stamps = null turns them off.
+int fmrx_debug_mono_stamps(fmrx_ctx* c, unsigned long long* d_stamps, size_t n_workgroups, size_t* needed) {
+    CtxLock lock_(c);
+    if (!c) return fail(FMRX_EINVAL, "null context");
+    if (needed) *needed = (size_t)c->cfg.n_streams * 256 * (size_t)mono_wg_per_cu(c->geo.rf_decim);
+    if (d_stamps && needed && n_workgroups < *needed)
+        return fail(FMRX_EINVAL, "stamp buffer holds %zu workgroups, up to %zu launch", n_workgroups, *needed);
+    c->stamps = d_stamps;
+    return FMRX_OK;
+}

@@ -52,6 +52,7 @@ struct MonoLaunch {
     long long n_if;             // IF samples per stream this call
     int segs;                   // workgroups (segments) per stream
     int audio;                  // 1: run the audio stage (pcm / mono outputs)
+    unsigned long long* stamps; // diagnostic (fmrx_debug_mono_stamps): 6 u64 per workgroup, else null
 };
 
 // Halo bytes the fused kernel needs in front of a call (pre-roll chunk + RF history).
@@ -139,8 +140,22 @@ int launch_psd(const float* x, int nseg, int N, const float* hann, double scale,
 // ---- generic filter.h primitives ------------------------------------------------------
 int launch_resample(float* out, const float* state, const float* in, int n_in,
                     const float* coeff, int taps, int up, int down, int n_out, hipStream_t s);
-int launch_polyphase(float* out, const float* state, const float* in, const float* coeff, int taps, int up,
-                     int down, int n_out, hipStream_t s);
+// mono audio stage of every stream in one launch (project.cpp:146 + the S16 quantiser)
+struct PolyStreams {
+    const float* in;        // stream s: in + s in_stride, n_out outputs' inputs
+    size_t in_stride;
+    const float* state;     // stream s: state + s state_stride, taps - 1 floats of history
+    size_t state_stride;
+    const float* coeff;     // taps
+    int taps, up, down, n_out;
+    float* out;             // optional float output (stream s at out + s out_stride)
+    size_t out_stride;
+    int16_t* pcm;           // S16 output (stream s at pcm + s pcm_stride)
+    size_t pcm_stride;
+};
+int launch_polyphase(const PolyStreams& P, int n_streams, hipStream_t s);
+int launch_copy_streams(float* dst, size_t dst_stride, const float* src, size_t src_stride, int n, int n_streams,
+                        hipStream_t s);
 int launch_tail_copy(float* dst, const float* src, int n, hipStream_t s);
 int launch_fm_demod(float* out, float* prev, const float* i, const float* q, int n,
                     hipStream_t s);

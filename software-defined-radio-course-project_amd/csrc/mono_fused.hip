@@ -154,6 +154,13 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     const int c_full = (int)(L.stream_bytes / (2 * P));  // chunks lying wholly in the data
     const int c_tail = n_if >= kAH ? (int)((n_if - kAH) / CIF) : -2;  // chunks holding the last 50
     if (c0 >= c1) return;
+    // ABL & 64 (diagnostic build, results unchanged): shader-clock and 100 MHz stamps around
+    // the workgroup's work, written only to L.stamps (nothing in the kernel reads them)
+    unsigned long long st_t0 = 0, st_r0 = 0;
+    if constexpr ((ABL & 64) != 0) {
+        st_t0 = __builtin_amdgcn_s_memtime();
+        st_r0 = __builtin_amdgcn_s_memrealtime();
+    }
     const long long n_audio = n_if * AU / AD;
 
     const uint8_t* in = L.iq + (size_t)stream * L.stream_bytes;
@@ -462,6 +469,20 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         ar = ar1;
         if constexpr (kWin) slot = slot + 1 == GA ? 0 : slot + 1;
     }
+    if constexpr ((ABL & 64) != 0) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_ID: SIMD, CU, SE
+        const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
+        if (tid == 0 && L.stamps) {  // per-lane address: a plain vector store
+            unsigned long long* o = L.stamps + 6 * ((size_t)blockIdx.x + tid);
+            o[0] = st_t0;
+            o[1] = t1;
+            o[2] = st_r0;
+            o[3] = r1;
+            o[4] = hw;
+            o[5] = xcc;
+        }
+    }
 }
 
 template <int T, int D, int AD, int NT, int R, int PD, int TR = 0, int AU = 1>
@@ -538,18 +559,25 @@ int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_de
         return -1;
     }
     if (audio_up > 1) audio_down = 5;  // RF + demod only (stereo engine, split API): any compiled AD
+    // clock / occupancy stamps (fmrx_debug_mono_stamps): the default kernel plus stamps
+    if (L.stamps && rf_taps == 101 && rf_decim == 10 && audio_down == 5 && vi == kDefaultVariant)
+        return launch_ablation<64>(L, n_streams, taps, s);
     if (const int a = ablation(); a != 0 && rf_taps == 101 && rf_decim == 10) {
         switch (a) {
             case 1: return launch_ablation<1>(L, n_streams, taps, s);
             case 2: return launch_ablation<2>(L, n_streams, taps, s);
             case 4: return launch_ablation<4>(L, n_streams, taps, s);
+            case 6: return launch_ablation<6>(L, n_streams, taps, s);
             case 8: return launch_ablation<8>(L, n_streams, taps, s);
+            case 14: return launch_ablation<14>(L, n_streams, taps, s);
             case 15: return launch_ablation<15>(L, n_streams, taps, s);
             case 16: return launch_ablation<16>(L, n_streams, taps, s);
             case 30: return launch_ablation<30>(L, n_streams, taps, s);
+            case 32: return launch_ablation<32>(L, n_streams, taps, s);
             case 31: return launch_ablation<31>(L, n_streams, taps, s);
             case 62: return launch_ablation<62>(L, n_streams, taps, s);
             case 63: return launch_ablation<63>(L, n_streams, taps, s);
+            case 64: return launch_ablation<64>(L, n_streams, taps, s);
             default: break;
         }
     }

@@ -37,16 +37,20 @@ __global__ void resample_kernel(float* __restrict__ out, const float* __restrict
 // floor(n down / up); its taps are coeff[k0 + i up] against in[j0 - i], i ascending (= k
 // ascending, as filter.cpp:84-92).  One division per output instead of one per tap; the
 // prototype keeps its order, so at tap step i a wave's lanes read inside one up-wide window.
-__global__ void polyphase_kernel(float* __restrict__ out, const float* __restrict__ state,
-                                 const float* __restrict__ in, const float* __restrict__ coeff,
-                                 int taps, int up, int down, int n_out) {
+// All streams in one launch (grid.y = stream); the S16 quantiser (project.cpp:185-191) is
+// fused, the float output is written only when the caller asks for it (out != nullptr).
+__global__ void polyphase_kernel(PolyStreams P) {
     const int n = blockIdx.x * blockDim.x + threadIdx.x;
-    if (n >= n_out) return;
-    const long long nd = (long long)n * down;
+    const int s = blockIdx.y;
+    if (n >= P.n_out) return;
+    const float* in = P.in + (size_t)s * P.in_stride;
+    const float* state = P.state + (size_t)s * P.state_stride;
+    const int taps = P.taps, up = P.up;
+    const long long nd = (long long)n * P.down;
     const long long j0 = nd / up;
     const int k0 = (int)(nd - j0 * up);
     const int cnt = (taps - k0 + up - 1) / up;  // taps of this phase: k0 + i up < taps
-    const float* c = coeff + k0;
+    const float* c = P.coeff + k0;
     float acc = 0.0f;
     if (cnt == 51 && j0 >= 50) {
         // every phase of the modes 2/3 prototypes (7497 = 51 x 147, 22491 = 51 x 441): a
@@ -71,7 +75,17 @@ __global__ void polyphase_kernel(float* __restrict__ out, const float* __restric
             acc = acc + p;
         }
     }
-    out[n] = acc;
+    if (P.out) P.out[(size_t)s * P.out_stride + n] = acc;
+    P.pcm[(size_t)s * P.pcm_stride + n] = quantize_s16(acc);
+}
+
+// dst[s][i] = src[s][i], i < n, every stream in one launch (grid.y = stream).  dst and src
+// may share a buffer (the demod history move) as long as the ranges do not overlap.
+__global__ void copy_streams_kernel(float* __restrict__ dst, size_t dst_stride, const float* __restrict__ src,
+                                    size_t src_stride, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = blockIdx.y;
+    if (i < n) dst[(size_t)s * dst_stride + i] = src[(size_t)s * src_stride + i];
 }
 
 __global__ void copy_kernel(float* __restrict__ dst, const float* __restrict__ src, int n) {
@@ -169,11 +183,17 @@ int launch_resample(float* out, const float* state, const float* in, int n_in,
     return ok();
 }
 
-int launch_polyphase(float* out, const float* state, const float* in, const float* coeff, int taps, int up,
-                     int down, int n_out, hipStream_t s) {
-    if (n_out <= 0) return 0;
-    hipLaunchKernelGGL(polyphase_kernel, dim3(blocks_for(n_out, 256)), dim3(256), 0, s, out, state, in, coeff,
-                       taps, up, down, n_out);
+int launch_polyphase(const PolyStreams& P, int n_streams, hipStream_t s) {
+    if (P.n_out <= 0 || n_streams <= 0) return 0;
+    hipLaunchKernelGGL(polyphase_kernel, dim3(blocks_for(P.n_out, 256), n_streams), dim3(256), 0, s, P);
+    return ok();
+}
+
+int launch_copy_streams(float* dst, size_t dst_stride, const float* src, size_t src_stride, int n, int n_streams,
+                        hipStream_t s) {
+    if (n <= 0 || n_streams <= 0) return 0;
+    hipLaunchKernelGGL(copy_streams_kernel, dim3(blocks_for(n, 256), n_streams), dim3(256), 0, s, dst, dst_stride,
+                       src, src_stride, n);
     return ok();
 }
 

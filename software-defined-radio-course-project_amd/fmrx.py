@@ -83,6 +83,7 @@ PROTOTYPES = {
     "fmrx_synth_host": (C.c_int, [C.c_uint64, C.c_int, C.c_uint64, _sz, _vp]),
     "fmrx_synth_device": (C.c_int, [_vp, C.c_uint64, C.c_int, C.c_uint64, _sz, _vp]),
     "fmrx_test_pll_fallback": (C.c_int, [_vp, C.c_int, _vp, _vp, _sz, _vp]),
+    "fmrx_debug_mono_stamps": (C.c_int, [_vp, _vp, _sz, C.POINTER(_sz)]),
 }
 
 _lib = None
@@ -342,6 +343,13 @@ class Receiver:
     def test_pll_fallback(self, kind: int, d_a, d_b, n: int, d_out) -> None:
         """Test hook: the PLL's fallback libm on device (0 sincos, 1 atan2, 2 NCO cos)."""
         _check(lib().fmrx_test_pll_fallback(self.h, kind, d_a, d_b, n, d_out))
+
+    def debug_mono_stamps(self, d_stamps: int | None, n_workgroups: int = 0) -> int:
+        """Diagnostic clock stamps of the fused mono kernel (fmrx.h); returns the stamp slots a
+        call may need (6 u64 each)."""
+        need = _sz()
+        _check(lib().fmrx_debug_mono_stamps(self.h, d_stamps, n_workgroups, C.byref(need)))
+        return need.value
 
 
 def build() -> None:

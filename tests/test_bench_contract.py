@@ -40,6 +40,12 @@ def test_bench_json_contract():
     assert 0 < rf["frac"] < 1 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
     # value = IQ pairs of the whole job / wall time; the kernel alone is faster than a step
     assert j["value"] > 1e5 and rf["kernel_ms"] <= j["ms_per_step"] * 1.05
+    # the binding roof next to HBM; per-GPU and aggregate rates spelled out
+    assert rf["binding"]["bound"] == "valu_f32_no_fma" and 0 < rf["binding"]["frac"] < 1
+    assert j["aggregate_MS_s"] == j["value"] and j["per_gpu_MS_s"] == round(j["value"] / j["n_gpus"], 1)
+    # traffic only with the stamp of the kernel sources that ran
+    if rf["traffic"] is not None:
+        assert rf["traffic_source"]
 
 
 def test_bench_cpu_baseline_keys():
@@ -47,3 +53,7 @@ def test_bench_cpu_baseline_keys():
     cb = j["cpu_baseline"]
     assert cb["kind"] in ("reference", "port") and cb["cores"] == 1 and cb["value"] > 0
     assert cb["bit_exact_vs_gpu"] is True
+    for key in ("cpu_baseline", "cpu_baseline_all_cores"):
+        h = j[key]["host"]
+        assert h["nproc"] >= 1 and h["cpu_model"] and 1 <= h["usable_cores"] <= h["affinity_cpus"]
+    assert j["cpu_baseline_all_cores"]["cores"] == j["cpu_baseline_all_cores"]["host"]["usable_cores"]

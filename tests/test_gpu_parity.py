@@ -114,6 +114,59 @@ def test_mono_call_split_and_resume(fmrx, orc, mode, rf_taps):
         assert np.array_equal(np.concatenate(parts), want)
 
 
+@pytest.mark.parametrize("mode,nb", [(0, 23), (1, 19), (2, 5)])
+def test_stereo_call_split_and_resume(fmrx, orc, mode, nb):
+    """REF_EXACT stereo across ragged call sizes and a checkpoint / resume into a second
+    context: the blob carries the demod history, PLL state, mixer tail and mono delay line of
+    every stream (3 streams, each its own input)."""
+    bb, rf_fs = oracle.MODES[mode][0], oracle.MODES[mode][3]
+    ns = 3
+    iqs = [iqgen.make(f"synth:{71 + k}", nb * bb, rf_fs) for k in range(ns)]
+    want = np.stack([orc.run(mode, 51, x, ["pcm"])["pcm"] for x in iqs])
+    iq = np.stack(iqs)
+    with fmrx.Receiver(mode, fmrx.STEREO, n_streams=ns) as rx:
+        ps = rx.geo.pcm_samples
+        parts, pos = [], 0
+        for n in (1, 3, 2, nb - 6):
+            parts.append(rx.process(iq[:, pos * bb:(pos + n) * bb]))
+            pos += n
+            if pos in (1, 4):  # checkpoint / resume through a second context
+                blob = rx.get_state()
+                with fmrx.Receiver(mode, fmrx.STEREO, n_streams=ns) as rx2:
+                    rx2.set_state(blob)
+                    tail = rx2.process(iq[:, pos * bb:])
+                assert np.array_equal(tail, want[:, pos * ps:]), (mode, pos)
+        assert np.array_equal(np.concatenate(parts, axis=1), want)
+
+
+def test_create_refuses_streams_beyond_grid_limit(fmrx):
+    """n_streams lands on grid.y of every per-stream launch: fmrx_create refuses a count no
+    device can launch (EINVAL at create time, before any allocation)."""
+    with pytest.raises(fmrx.FmrxError) as e:
+        fmrx.Receiver(0, fmrx.STEREO, n_streams=2**31 - 1)
+    assert e.value.code == fmrx.FMRX_EINVAL
+
+
+def test_state_blob_keeps_seek_staleness(fmrx):
+    """A blob taken between fmrx_seek and the next fused call restores a stale audio history:
+    the split API's audio stage must refuse it in the second context too (ESTATE)."""
+    bb = oracle.MODES[0][0]
+    iq = iqgen.make("synth:5", 3 * bb)
+    with fmrx.Receiver(0, fmrx.MONO) as rx:
+        rx.process(iq[:bb])
+        rx.seek(iq[:2 * bb])
+        blob = rx.get_state()
+        demod = np.zeros(rx.geo.if_samples, np.float32)
+        with pytest.raises(fmrx.FmrxError):
+            rx.audio_block(demod)
+        with fmrx.Receiver(0, fmrx.MONO) as rx2:
+            rx2.set_state(blob)
+            with pytest.raises(fmrx.FmrxError):
+                rx2.audio_block(demod)
+            rx2.process(iq[2 * bb:])  # a fused call refreshes the history
+            rx2.audio_block(demod)
+
+
 @pytest.mark.parametrize("mode,nb", [(2, 6), (3, 4)])
 def test_polyphase_mono_split_resume_and_mixed_api(fmrx, orc, mode, nb):
     """Modes 2/3 run the rational resampler inside the fused kernel; its history must survive

@@ -13,4 +13,6 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/pmc_fetch -o run --outpu
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-other-configs > $OUT/pmc_fetch.log 2>&1 || exit 3
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/pmc_write -o run --output-format csv -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-other-configs > $OUT/pmc_write.log 2>&1 || exit 4
+timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT -T -d $OUT/pmc_grbm -o run --output-format csv -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-other-configs > $OUT/pmc_grbm.log 2>&1 || exit 5
 echo done

@@ -10,6 +10,11 @@ import os
 import shutil
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402  (kernel_source_hash: the stamp bench.py checks)
+
+BENCH_HASH = bench.kernel_source_hash()
+
 tag, dest = sys.argv[1], sys.argv[2]
 src = f"gpurun_out/{tag}"
 out = f"profiles/{dest}"
@@ -30,12 +35,30 @@ for f, key in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
             w.writerow([r["Kernel_Name"][:60], r["Counter_Name"], r["Counter_Value"],
                         int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), r["Grid_Size"], r["Workgroup_Size"],
                         r["LDS_Block_Size"], r["VGPR_Count"], r["SGPR_Count"]])
-bench = json.load(open(f"{src}/bench.json"))
-alg = bench["roofline"]["alg_bytes_per_launch"]
+# effective clock (MI355X_MICROARCH.md, DVFS give-back): GRBM_GUI_ACTIVE summed over the 8 XCDs
+# / 8 / the dispatch's own duration, per fused launch of the GRBM pass
+clk = None
+if os.path.exists(f"{src}/pmc_grbm/run_counter_collection.csv"):
+    rows = [r for r in csv.DictReader(open(f"{src}/pmc_grbm/run_counter_collection.csv"))
+            if "mono_fused" in r["Kernel_Name"] and r["Counter_Name"] == "GRBM_GUI_ACTIVE"]
+    ghz = [float(r["Counter_Value"]) / 8 / (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in rows]
+    if ghz:
+        clk = round(sorted(ghz)[len(ghz) // 2], 3)
+        with open(f"{out}/pmc_grbm_mono_fused.csv", "w") as g:
+            w = csv.writer(g)
+            w.writerow(["Kernel_Name", "Counter_Name", "Counter_Value", "DurationNs", "effective_clock_GHz"])
+            for r, c in zip(rows, ghz):
+                w.writerow([r["Kernel_Name"][:60], r["Counter_Name"], r["Counter_Value"],
+                            int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), round(c, 4)])
+bline = json.load(open(f"{src}/bench.json"))
+alg = bline["roofline"]["alg_bytes_per_launch"]
 fetch = res["FETCH_SIZE_kb_per_launch"] * 1024 * 2  # gfx950: FETCH_SIZE counts half of a coalesced stream
 write = res["WRITE_SIZE_kb_per_launch"] * 1024
 res.update({
-    "kernel": bench["roofline"]["kernel"], "workload": "1 GiB mode-0 mono, 101-tap RF (bench.py)",
+    "kernel": bline["roofline"]["kernel"], "kernel_source_sha256": BENCH_HASH,
+    "effective_clock_ghz": clk,
+    "clock_note": "median over the GRBM pass's fused launches of GRBM_GUI_ACTIVE / 8 / duration" if clk else None,
+    "workload": "1 GiB mode-0 mono, 101-tap RF (bench.py)",
     "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE "
                   "counts half the bytes of a coalesced stream; units KiB)",
     "hbm_read_bytes_per_launch": int(fetch), "hbm_write_bytes_per_launch": int(write),
