@@ -98,6 +98,19 @@ def host_info() -> dict:
             "cpu_share_env": share, "usable_cores": usable}
 
 
+def warm_up(step, sync, n_steps: int, min_seconds: float) -> int:
+    """Untimed steps: n_steps, continuing until min_seconds of back-to-back work have passed.
+    Returns the number of steps run."""
+    t0 = time.perf_counter()
+    done = 0
+    while done < n_steps or time.perf_counter() - t0 < min_seconds:
+        for _ in range(min(64, n_steps - done) if done < n_steps else 64):
+            step()
+            done += 1
+        sync()
+    return done
+
+
 def flops_per_iq(rf_taps: int) -> float:
     # per IQ pair (SURVEY §8a): RF 2 ch x taps x (mul+add) / 10, demod ~9/10, audio 51x2/50
     return 2 * rf_taps * 2 / 10 + 0.9 + 51 * 2 / 50
@@ -108,6 +121,8 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--min-warmup-seconds", type=float, default=1.0,
+                    help="untimed warm-up runs at least this long (clock ramp), besides the W steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-bytes", type=int, default=STREAM_BYTES)
     ap.add_argument("--no-other-configs", action="store_true",
@@ -154,9 +169,12 @@ def main() -> None:
         if dist is not None:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        rx.process_device(d_iq.data_ptr(), nb, d_pcm.data_ptr())
-    rx.synchronize()
+    # Untimed warm-up: W steps, and at least --min-warmup-seconds of back-to-back steps.  The
+    # MI355X raises its clock over ~0.5 s of sustained load (profiles/r02/warmup/: the same
+    # kernel takes 0.66 ms per GiB after 3 warm-up steps and 0.57 ms once the clock has ramped,
+    # the same 0.57 ms over 1,500 timed steps), so the timed K steps measure the sustained rate.
+    warmup_steps_run = warm_up(lambda: rx.process_device(d_iq.data_ptr(), nb, d_pcm.data_ptr()), rx.synchronize,
+                               args.warmup, args.min_warmup_seconds)
     rx.kernel_timing(reset=1)  # arm per-launch HIP events on the context stream
     barrier()
     torch.cuda.synchronize()
@@ -186,6 +204,7 @@ def main() -> None:
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warmup_steps_run": warmup_steps_run,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
@@ -293,9 +312,7 @@ def other_configs(fmrx) -> dict:
         iq = torch.empty(nb * bb, dtype=torch.uint8, device="cuda")
         pcm = torch.empty(nb * rx.geo.pcm_samples, dtype=torch.int16, device="cuda")
         rx.synth_device(3001, 0, nb * bb // 2, iq.data_ptr())
-        for _ in range(2):
-            rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
-        rx.synchronize()
+        warm_up(lambda: rx.process_device(iq.data_ptr(), nb, pcm.data_ptr()), rx.synchronize, 2, 1.0)
         steps = 10
         t0 = time.perf_counter()
         for _ in range(steps):

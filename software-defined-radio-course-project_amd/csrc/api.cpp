@@ -242,6 +242,26 @@ int mono_segments(const fmrx_ctx* c, long long n_if) {
     return (int)std::max<long long>(1, segs);
 }
 
+// Unequal shares for the two waves of a SIMD (mono_fused.hip mono_share): when the grid is
+// two resident waves per SIMD (segs even, >= 15/16 of 2 x the SIMD count, 8 workgroups per
+// CU), the first-dispatched wave takes kOlderShare/1024 of each span.  FMRX_MONO_SPLIT=<n>
+// overrides it (0 = equal segments; timing sweeps).
+constexpr int kOlderShare = 620;
+int mono_older_share(const fmrx_ctx* c, int segs) {
+    static const int n_simd = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return 4 * cus;
+    }();
+    int share = kOlderShare;
+    if (const char* e = std::getenv("FMRX_MONO_SPLIT")) share = std::atoi(e);
+    if (share <= 0 || share >= 1024) return 0;
+    const long long wgs = (long long)segs * c->cfg.n_streams;
+    if ((segs & 1) != 0 || mono_wg_per_cu(c->geo.rf_decim) != 8 || wgs * 16 < 2LL * n_simd * 15 || wgs > 2LL * n_simd)
+        return 0;
+    return share;
+}
+
 // RF front end (+ the mono audio stage when `pcm` is non-null and the mode allows it).
 int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm, float* d_mono,
               float* d_demod, size_t demod_stride, int demod_hist, bool with_audio) {
@@ -266,6 +286,7 @@ int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
     L.halo_bytes = c->halo_bytes;
     L.n_if = (long long)(n_blocks * c->geo.if_samples);
     L.segs = mono_segments(c, L.n_if);
+    L.older_share = mono_older_share(c, L.segs);
     L.stamps = c->stamps;
     L.audio = with_audio ? 1 : 0;
     const int ad = c->geo.audio_up == 1 ? c->geo.audio_down : 5;

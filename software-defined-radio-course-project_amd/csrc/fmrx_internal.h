@@ -53,6 +53,8 @@ struct MonoLaunch {
     int segs;                   // workgroups (segments) per stream
     int audio;                  // 1: run the audio stage (pcm / mono outputs)
     unsigned long long* stamps; // diagnostic (fmrx_debug_mono_stamps): 6 u64 per workgroup, else null
+    int older_share;            // 0: equal segments; else (even segs, two waves per SIMD) the
+                                //   first-dispatched wave's share of a SIMD's span, in 1/1024
 };
 
 // Halo bytes the fused kernel needs in front of a call (pre-roll chunk + RF history).

@@ -105,6 +105,33 @@ __device__ inline float sbyte(uint32_t w) {
     return f;
 }
 
+// Workgroup -> (stream, chunk range).  Uniform: segment blockIdx % segs of stream
+// blockIdx / segs.  With L.older_share (> 0, in 1/1024; even segs): the grid is two waves per
+// SIMD, and the hardware dispatches workgroup w into the first wave slot of its SIMD and
+// w + grid/2 into the second; the first-dispatched wave wins VALU arbitration (measured on
+// MI355X: in 1,024 of 1,024 SIMD pairs it finished first, ~410 vs ~571 us with equal shares,
+// profiles/r02/mono_stamps_*.json).  So w and w + grid/2 split one span of one stream, w
+// taking older_share/1024 of it, and both finish together.  Every chunk is still covered
+// exactly once and each range starts with its own pre-roll, so the output is unchanged.
+__device__ inline void mono_share(const MonoLaunch& L, int w, int n_chunks, int* stream, int* c0, int* c1) {
+    if (L.older_share > 0) {
+        const int half = L.segs / 2;              // span pairs per stream
+        const int H = (int)gridDim.x / 2;         // = n_streams * half
+        const int p = w < H ? w : w - H;          // pair index
+        const int s = p / half, q = p - s * half;
+        const int p0 = (int)((long long)q * n_chunks / half), p1 = (int)((long long)(q + 1) * n_chunks / half);
+        const int cut = p0 + (int)(((long long)(p1 - p0) * L.older_share) >> 10);
+        *stream = s;
+        *c0 = w < H ? p0 : cut;
+        *c1 = w < H ? cut : p1;
+        return;
+    }
+    *stream = w / L.segs;
+    const int seg = w - *stream * L.segs;
+    *c0 = (int)((long long)seg * n_chunks / L.segs);
+    *c1 = (int)((long long)(seg + 1) * n_chunks / L.segs);
+}
+
 // ABL (timing ablations only, never selected in production): bit 1 skips the RF FIR, 2 the
 // audio FIR, 4 the demod, 8 the byte conversion of the staging, 16 the global loads, 32 the
 // staging writes.
@@ -143,14 +170,12 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     };
 
     const int tid = threadIdx.x;
-    const int stream = blockIdx.x / L.segs;
-    const int seg = blockIdx.x - stream * L.segs;
     const long long n_if = L.n_if;
     // chunk indices fit 32 bits for any HBM-resident stream (n_if / CIF < 2^31); positions
     // in the stream stay 64-bit
     const int n_chunks = (int)((n_if + CIF - 1) / CIF);
-    const int c0 = (int)((long long)seg * n_chunks / L.segs);
-    const int c1 = (int)((long long)(seg + 1) * n_chunks / L.segs);
+    int stream, c0, c1;
+    mono_share(L, (int)blockIdx.x, n_chunks, &stream, &c0, &c1);
     const int c_full = (int)(L.stream_bytes / (2 * P));  // chunks lying wholly in the data
     const int c_tail = n_if >= kAH ? (int)((n_if - kAH) / CIF) : -2;  // chunks holding the last 50
     if (c0 >= c1) return;

@@ -23,6 +23,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--warm-seconds", type=float, default=2.0)
+    ap.add_argument("--idle", action="store_true", help="stamp a launch that follows a sync (boost clock)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -47,9 +48,17 @@ def main():
             rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
         rx.synchronize()
         launches += 50
+    # steady state: the stamped launch is the last of 40 back-to-back launches (no idle gap
+    # in front of it, as in bench.py's timed loop); --idle stamps a launch after a sync instead
+    if not args.idle:
+        for _ in range(40):
+            rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
+        launches += 40
     rx.debug_mono_stamps(st.data_ptr(), need)
+    rx.kernel_timing(reset=1)  # HIP events around the stamped launch on the context stream
     rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
     rx.synchronize()
+    ev_ms, _ = rx.kernel_timing(reset=-1)
     rx.debug_mono_stamps(None)
     a = st.cpu().numpy().reshape(-1, 6).astype(np.int64)
     a = a[a[:, 3] > 0]  # workgroups that ran
@@ -59,11 +68,13 @@ def main():
     life = (r1 - r0) * 10.0
     out = {
         "workload": "bench.py configs[1]: mode-0 mono, 101-tap RF, 1 GiB, one stamped launch after "
-                    f"{launches} warm launches ({args.warm_seconds} s)",
+                    f"{launches} warm launches ({args.warm_seconds} s), "
+                    + ("after a sync (idle in front)" if args.idle else "the last of 41 back-to-back launches"),
         "workgroups": int(len(a)),
         "clock_ghz_median": round(float(np.median(clk)), 3),
         "clock_ghz_p05_p95": [round(float(np.percentile(clk, 5)), 3), round(float(np.percentile(clk, 95)), 3)],
         "launch_span_us": round(span / 1e3, 2),
+        "hip_event_kernel_us": round(ev_ms * 1e3, 2),
         "wg_lifetime_us_median": round(float(np.median(life)) / 1e3, 2),
         "wg_lifetime_over_span_mean": round(float(life.mean() / span), 4),
         "start_spread_us": round(float((r0.max() - r0.min()) * 10.0) / 1e3, 2),

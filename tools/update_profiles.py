@@ -20,6 +20,17 @@ src = f"gpurun_out/{tag}"
 out = f"profiles/{dest}"
 os.makedirs(out, exist_ok=True)
 shutil.copy(f"{src}/kt/run_kernel_stats.csv", f"{out}/kernel_stats.csv")
+# the traced bench's timed launches are its last `steps` fused launches (the untimed warm-up
+# runs >= 1 s first): their mean duration is what bench.py's kernel_ms measures
+trace = [r for r in csv.DictReader(open(f"{src}/kt/run_kernel_trace.csv")) if "mono_fused" in r["Kernel_Name"]]
+trace.sort(key=lambda r: int(r["Start_Timestamp"]))
+kt_steps = 10  # tools/gpu_bench_prof.sh traces bench.py --steps 10
+last = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace[-kt_steps:]]
+with open(f"{out}/kernel_trace_timed_launches.json", "w") as g:
+    json.dump({"kernel": "mono_fused_kernel", "launches_traced": len(trace), "timed_launches": len(last),
+               "timed_mean_ns": sum(last) / len(last), "timed_ns": last,
+               "note": "rocprofv3 --kernel-trace of bench.py --steps 10: the last 10 fused launches are the timed "
+                       "ones (kernel_stats.csv averages every launch, warm-up included)"}, g, indent=1)
 shutil.copy(f"{src}/bench.json", f"{out}/bench.json")
 res = {}
 for f, key in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
