@@ -98,6 +98,27 @@ def host_info() -> dict:
             "cpu_share_env": share, "usable_cores": usable}
 
 
+def hbm_copy_bandwidth(src, reps: int = 20) -> float:
+    """GB/s of a device-to-device copy of `src` (bytes read + bytes written), median of reps."""
+    import torch
+
+    dst = torch.empty_like(src)
+    for _ in range(3):
+        dst.copy_(src)
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        dst.copy_(src)
+        b.record()
+        b.synchronize()
+        times.append(a.elapsed_time(b) * 1e-3)
+    del dst
+    times.sort()
+    return round(2 * src.numel() * src.element_size() / times[len(times) // 2] / 1e9, 1)
+
+
 def warm_up(step, sync, n_steps: int, min_seconds: float) -> int:
     """Untimed steps: n_steps, continuing until min_seconds of back-to-back work have passed.
     Returns the number of steps run."""
@@ -240,6 +261,10 @@ def main() -> None:
             "flop_per_iq": round(flops_per_iq(RF_TAPS), 2),
         },
     }
+    # the attainable HBM bandwidth next to the datasheet peak -- a device-to-device
+    # copy of the 1 GiB input (read + write counted), after the timed region
+    line["roofline"]["hbm_attainable_GBs"] = hbm_copy_bandwidth(d_iq)
+    line["roofline"]["frac_of_attainable"] = round(achieved / line["roofline"]["hbm_attainable_GBs"], 4)
     # binding roof: the kernel is bound by the FP32 VALU without FMA (bit parity), not by HBM
     line["roofline"]["binding"] = dict(line["compute"])
     # PMC traffic of record, only while it was measured on this kernel's sources

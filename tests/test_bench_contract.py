@@ -43,6 +43,8 @@ def test_bench_json_contract():
     # the binding roof next to HBM; per-GPU and aggregate rates spelled out
     assert rf["binding"]["bound"] == "valu_f32_no_fma" and 0 < rf["binding"]["frac"] < 1
     assert j["aggregate_MS_s"] == j["value"] and j["per_gpu_MS_s"] == round(j["value"] / j["n_gpus"], 1)
+    # the attainable HBM bandwidth (device copy) sits below the datasheet peak
+    assert 1000 < rf["hbm_attainable_GBs"] < 1.1 * rf["peak"]
     # traffic only with the stamp of the kernel sources that ran
     if rf["traffic"] is not None:
         assert rf["traffic_source"]

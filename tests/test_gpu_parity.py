@@ -214,6 +214,25 @@ def test_mono_multistream_independent(fmrx, orc):
         assert np.array_equal(out[s], orc.run(0, 101, iq, ["pcm_mono"])["pcm_mono"]), s
 
 
+@pytest.mark.parametrize("channels,n_streams,share", [(1, 3, None), (1, 4, "900"), (2, 2, None)])
+def test_unequal_wave_shares_multistream(fmrx, orc, monkeypatch, channels, n_streams, share):
+    """The fused kernel's two-waves-per-SIMD split (mono_fused.hip mono_share: workgroups w and
+    w + grid/2 share a span, the first taking kOlderShare/1024 of it) with several streams:
+    ~2,048 workgroups (3 streams: 682 even segments each, 2,046 workgroups), an extreme share
+    (FMRX_MONO_SPLIT=900), and the stereo engine's front end.  Every stream equals the oracle."""
+    if share is not None:
+        monkeypatch.setenv("FMRX_MONO_SPLIT", share)
+    nb, bb = 420, 12800  # 2,800 chunks per stream: enough for the full-chip grid
+    recipes = [("synth:%d" if s % 2 == 0 else "rand:%d") % (300 + s) for s in range(n_streams)]
+    ins = np.stack([iqgen.make(r, nb * bb) for r in recipes])
+    taps = 101 if channels == 1 else 51
+    with fmrx.Receiver(0, channels, rf_taps=taps, n_streams=n_streams) as rx:
+        out = rx.process(ins)
+    field = "pcm" if channels == 2 else "pcm_mono"
+    for s_ in range(n_streams):
+        assert np.array_equal(out[s_], orc.run(0, taps, ins[s_], [field])[field]), s_
+
+
 @pytest.mark.parametrize("mode,rf_taps,nb,cuts", [(0, 101, 40, (1, 7, 23)), (0, 51, 12, (3,)),
                                                    (1, 51, 30, (2, 17)), (2, 51, 4, (1, 3)), (3, 101, 3, (1, 2))])
 def test_time_shards_with_seek_equal_whole_stream(fmrx, mode, rf_taps, nb, cuts):
