@@ -289,6 +289,12 @@ int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
     L.older_share = mono_older_share(c, L.segs);
     L.stamps = c->stamps;
     L.audio = with_audio ? 1 : 0;
+    // the halo update rides in the fused kernel when every stream row is 16-B aligned (halo
+    // bytes and block bytes are multiples of 16); otherwise halo_kernel runs after it
+    const char* he = std::getenv("FMRX_HALO_KERNEL");  // =1: the separate halo_kernel (A/B timing)
+    const bool fused_halo = (reinterpret_cast<uintptr_t>(d_iq) & 15) == 0 && L.stream_bytes % 16 == 0 &&
+                            c->halo_bytes % 16 == 0 && !(he && he[0] == '1');
+    L.halo_next = fused_halo ? c->d_halo[c->halo_cur ^ 1].p : nullptr;
     const int ad = c->geo.audio_up == 1 ? c->geo.audio_down : 5;
     std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
     if (c->timing) {
@@ -306,9 +312,11 @@ int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
     if (rc != 0) return fail(rc == -1 ? FMRX_EINVAL : FMRX_EHIP, "fused kernel launch failed (%d)", rc);
     if (ev) HIPCHK(hipEventRecord(ev->second, c->stream));
     if (with_audio) c->audio_hist_stale = false;  // demod_tail rewrote the audio history
-    rc = launch_halo_update(d_iq, L.stream_bytes, c->d_halo[c->halo_cur].p,
-                            c->d_halo[c->halo_cur ^ 1].p, c->halo_bytes, ns, c->stream);
-    if (rc != 0) return fail(FMRX_EHIP, "halo update failed");
+    if (!fused_halo) {
+        rc = launch_halo_update(d_iq, L.stream_bytes, c->d_halo[c->halo_cur].p, c->d_halo[c->halo_cur ^ 1].p,
+                                c->halo_bytes, ns, c->stream);
+        if (rc != 0) return fail(FMRX_EHIP, "halo update failed");
+    }
     c->halo_cur ^= 1;
     return 0;
 }

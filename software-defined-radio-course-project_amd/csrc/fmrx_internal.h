@@ -55,6 +55,9 @@ struct MonoLaunch {
     unsigned long long* stamps; // diagnostic (fmrx_debug_mono_stamps): 6 u64 per workgroup, else null
     int older_share;            // 0: equal segments; else (even segs, two waves per SIMD) the
                                 //   first-dispatched wave's share of a SIMD's span, in 1/1024
+    uint8_t* halo_next;         // optional: the halo after this call (last halo_bytes of halo ++
+                                //   iq per stream), written by the kernel in 16-B words; the
+                                //   caller guarantees 16-B aligned iq rows (else null + halo_kernel)
 };
 
 // Halo bytes the fused kernel needs in front of a call (pre-roll chunk + RF history).

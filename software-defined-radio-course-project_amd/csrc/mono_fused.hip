@@ -174,6 +174,17 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     // chunk indices fit 32 bits for any HBM-resident stream (n_if / CIF < 2^31); positions
     // in the stream stay 64-bit
     const int n_chunks = (int)((n_if + CIF - 1) / CIF);
+    // the next call's halo (halo_kernel's copy, fused): every workgroup moves a few 16-B words
+    // of the streams' tails; nothing in this launch reads halo_next
+    if (L.halo_next) {
+        const size_t words = L.halo_bytes / 16, total = words * (size_t)(gridDim.x / L.segs);
+        for (size_t i = (size_t)blockIdx.x * NT + tid; i < total; i += (size_t)gridDim.x * NT) {
+            const size_t s = i / words, j = i - s * words, v = L.stream_bytes + 16 * j;  // into halo ++ iq
+            const uint4 w = v < L.halo_bytes ? *reinterpret_cast<const uint4*>(L.halo + s * L.halo_bytes + v)
+                                             : *reinterpret_cast<const uint4*>(L.iq + s * L.stream_bytes + (v - L.halo_bytes));
+            *reinterpret_cast<uint4*>(L.halo_next + s * L.halo_bytes + 16 * j) = w;
+        }
+    }
     int stream, c0, c1;
     mono_share(L, (int)blockIdx.x, n_chunks, &stream, &c0, &c1);
     const int c_full = (int)(L.stream_bytes / (2 * P));  // chunks lying wholly in the data
