@@ -381,6 +381,7 @@ __global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, i
                 ld_d(pr, spr, bn, j / 2);
                 ld_d(hh, sh, bn, j / 2);
             }
+            __builtin_amdgcn_sched_barrier(0);  // see pll_spec_lane_kernel
         };
         float o[NB];
         (void)pll_batch_fast<NB, SPLIT, true>(p, ctx, v, iv, pr, o, Ki, Kp, refill, sc, hh);
@@ -391,6 +392,149 @@ __global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, i
             for (int q = 0; q < NB / 4; q++)
                 reinterpret_cast<float4*>(ob)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
             rec[(size_t)s * rb + b] = make_float2(p.integ, p.phase);
+        }
+    }
+}
+
+// ---- the speculative runner with lane roles (split layout, 16-lane rows) ---------------------
+//
+// pll_spec_kernel<SPLIT> already evaluates sin and cos as one polynomial on even / odd lanes.
+// This form gives a third lane of each row a job too: the two reductions of a step's trigArg
+// x -- r = x - nd pi/2 for sin/cos and the atan2 offset B = (m - h) 2 pi - x of the NEXT step
+// (pll_offset_h) -- are the same five operations with different constants,
+//     t = rint(fma(x, C1, H)) - H,   w = fma(-t, Clo, fma(-t, Chi, x)),
+// (C1, Chi, Clo, H) = (2/pi, pi/2 hi, pi/2 lo, 0) on the sin/cos lanes (w = r, bit for bit:
+// fma(x, C1, +0) is the rounded product) and (1/(2 pi), 2 pi hi, 2 pi lo, half turn) on lane 2
+// of the row (w = -B, bit for bit: fma is odd under negating an operand pair), so lane 2
+// computes the offset while the others compute r, and a third row broadcast hands -B to every
+// lane.  Every lane loads its stream's half turns; a per-lane mask zeroes them off lane 2.
+// The batch state (fc, nfs, sn, cs, -B) stays in registers from batch to batch; nothing on
+// the serial chain is a packed op (a packed f32 result read by the next instruction costs a
+// wait state on gfx950).  The result is checked by pll_check_kernel like pll_spec_kernel's.
+template <int L>
+__device__ inline double row_bcast(double v) {
+    const long long bits = __builtin_bit_cast(long long, v);
+    return __builtin_bit_cast(double, (long long)__builtin_amdgcn_mov_dpp(bits, 0x150 + L, 0xF, 0xF, false));
+}
+
+template <int NB, int LB>
+__global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int n, int n_streams, int spw,
+                                                           size_t stride, const double* side, size_t seg, double step,
+                                                           float norm_bw, const float* st, float* out_base,
+                                                           size_t ostride, int* fail, float2* rec, size_t rb,
+                                                           int inject) {
+    const int t = threadIdx.x & 63;
+    const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int s_lane = wave * spw + ((t >> 4) & (spw - 1));
+    const bool owner = (t & 15) == 0 && (t >> 4) < spw && s_lane < n_streams;
+    const bool b_lane = (t & 15) == 2;
+    const SplitCoef sc = split_coef((t & 1) != 0);
+    const double C1 = b_lane ? kInv2Pi : kInvPio2;
+    const double Chi = b_lane ? k2PiHi : kPio2Hi;
+    const double Clo = b_lane ? k2PiLo : kPio2Lo;
+    const int s = s_lane < n_streams ? s_lane : n_streams - 1;
+    const float* x = io + (size_t)s * stride;
+    float* out = out_base + (size_t)s * ostride;
+    const double2* siv = reinterpret_cast<const double2*>(side) + (size_t)s * (seg / 2);
+    const double2* spr = reinterpret_cast<const double2*>(side) + seg * (size_t)n_streams / 2 + (size_t)s * (seg / 2);
+    const double2* shl = reinterpret_cast<const double2*>(side) + seg * (size_t)n_streams + (size_t)s * (seg / 2);
+    // the half turn's high dword survives on lane 2 only (its low dword is 0 for 0.5 and 0)
+    const uint64_t hmask = ((uint64_t)(b_lane ? 0xFFFFFFFFu : 0u) << 32) | 0xFFFFFFFFull;
+    const float* S = st + 8 * (size_t)s;
+    const float Kp = norm_bw * static_cast<float>(2.666);
+    const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
+    PllState p{S[0], S[1], S[2], S[3], S[5]};
+    const int nb = n / NB;
+    if (owner) fail[s] = nb;
+    PllCtx ctx{};
+    ctx.valid = false;
+    if (nb > 0) {  // batch 0 on the exact path (see pll_spec_kernel)
+        const PllPair r = pll_redo(p, ctx, x, out, NB, Ki, Kp, step);
+        p = r.p;
+        ctx = r.ctx;
+        if (owner) rec[(size_t)s * rb] = make_float2(p.integ, p.phase);
+    }
+    if (nb < 2) return;
+    float v[NB];
+    double iv[NB], pr[NB], hz[NB];
+    auto ld_v = [&](int b, int q) {
+        *reinterpret_cast<float4*>(&v[4 * q]) = reinterpret_cast<const float4*>(x + b * NB)[q];
+    };
+    auto ld_d = [&](double (&dst)[NB], const double2* row, int b, int q) {
+        *reinterpret_cast<double2*>(&dst[2 * q]) = row[b * (NB / 2) + q];
+    };
+#pragma unroll
+    for (int q = 0; q < NB / 4; q++) ld_v(1, q);
+#pragma unroll
+    for (int q = 0; q < NB / 2; q++) {
+        ld_d(iv, siv, 1, q);
+        ld_d(pr, spr, 1, q);
+        ld_d(hz, shl, 1, q);
+    }
+    // the state of batch 1's first step, as pll_batch_fast starts (every lane alike)
+    const int q0 = ctx.q;
+    const float u0 = (q0 & 1) ? p.fbQ : p.fbI, w0 = (q0 & 1) ? p.fbI : -p.fbQ;
+    float fc = (q0 & 2) ? -u0 : u0, nfs = (q0 & 2) ? -w0 : w0;
+    double sn = ctx.sn, cs = ctx.cs;
+    double nB = -pll_offset_h(ctx.x, iv[0] < 0.0 ? 0.5 : 0.0);
+    float integ = p.integ, phase = p.phase;
+    for (int b = 1; b < nb; b++) {
+        const int bn = b + 1 < nb ? b + 1 : b;
+        float o[NB];
+#pragma unroll
+        for (int j = 0; j < NB; j++) {
+            const float a = v[j] * fc;
+            const float bb = v[j] * nfs;
+            const double Y = fma((double)a, sn, (double)bb * cs);
+            const float e = (float)fma(Y, iv[j], -nB);
+            const float ki_e = Ki * e;
+            const float kp_e = Kp * e;
+            integ = integ + ki_e;
+            phase = phase + (kp_e + integ);
+            const float arg = (float)(pr[j] + (double)phase);
+            o[j] = arg;
+            const double xa = (double)arg;
+            double w;
+            if constexpr (LB != 0) {
+                const double H = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, hz[(j + 1) % NB]) & hmask);
+                const double tq = rint(fma(xa, C1, H)) - H;
+                w = fma(-tq, Clo, fma(-tq, Chi, xa));  // r, or -B on lane 2
+                if constexpr (LB == 1) {
+                    nB = row_bcast<2>(w);
+                } else {  // one stream per wave: lane 2's value through two SGPRs
+                    const long long wb = __builtin_bit_cast(long long, w);
+                    const int lo = __builtin_amdgcn_readlane((int)wb, 2), hi = __builtin_amdgcn_readlane((int)(wb >> 32), 2);
+                    nB = __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+                }
+            } else {
+                const double nd = rint(xa * kInvPio2);
+                w = fma(-nd, kPio2Lo, fma(-nd, kPio2Hi, xa));
+                nB = -pll_offset_h(xa, hz[(j + 1) % NB]);
+            }
+            const double z = w * w;
+            const double W = split_w_horner(z, sc);
+            sn = row_bcast<0>(w * W);
+            cs = row_bcast<1>(W);
+            fc = (float)cs;
+            nfs = -(float)sn;
+            // refill after step j: v[j], iv[j], pr[j] and hz[j] (read at step j - 1) are dead
+            if (j % 4 == 3) ld_v(bn, j / 4);
+            if (j % 2 == 1) {
+                ld_d(iv, siv, bn, j / 2);
+                ld_d(pr, spr, bn, j / 2);
+                ld_d(hz, shl, bn, j / 2);
+            }
+            // keep each refill after the step that consumed its registers: hoisted loads
+            // would overlap the old values and cost a register copy per element a batch
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (inject >= 0 && b == 1 + (inject + s) % (nb - 1)) phase += 1.0e-3f;  // test hook: a wrong batch
+        if (owner) {
+            float* ob = out + b * NB;
+#pragma unroll
+            for (int q = 0; q < NB / 4; q++)
+                reinterpret_cast<float4*>(ob)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
+            rec[(size_t)s * rb + b] = make_float2(integ, phase);
         }
     }
 }
@@ -750,6 +894,11 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         return e ? std::atoi(e) : -1;
     }();
     const bool spec = spec_env && (reinterpret_cast<uintptr_t>(io) & 15) == 0 && stride % 4 == 0;
+    // FMRX_PLL_RUNNER=0: the runner without lane roles (A/B measurements)
+    const int lane_runner = [] {  // 1 lane roles (default), 2 the same without the offset lane
+        const char* e = std::getenv("FMRX_PLL_RUNNER");
+        return e ? std::atoi(e) : 1;
+    }();
     int spw = 1;
     while (spw < 64 && (long long)spw * n_simd < n_streams) spw *= 2;
     // Waves of 64 lanes; past 256 waves, workgroups of 4 waves, one per SIMD of a CU: 64-lane
@@ -757,6 +906,11 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     const int waves = (n_streams + spw - 1) / spw;
     const int wpg = waves > n_simd / 4 ? 4 : 1;
     const dim3 grid((waves + wpg - 1) / wpg), block(64 * wpg);
+    // FMRX_PLL_LDS (bytes, experiments): dynamic LDS per runner workgroup, to pin one per CU
+    static const unsigned runner_lds = [] {
+        const char* e = std::getenv("FMRX_PLL_LDS");
+        return e ? (unsigned)std::atoi(e) : 0u;
+    }();
     // filter.cpp:163: 2*PI*(freq/Fs) in double from the float quotient (host == device IEEE)
     const double step = (2.0 * 3.14159265358979323846) * static_cast<double>(freq / fs);  // dy4.h:14 PI
     for (size_t off = 0; off < (size_t)n; off += seg) {
@@ -771,11 +925,20 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         float* out = spec ? args : x;
         const size_t ostride = spec ? seg : stride;
         if (spec) {
-            if (spw <= 4)
-                hipLaunchKernelGGL((pll_spec_kernel<kPllBatch, true>), grid, block, 0, s, x, m, n_streams, spw,
+            if (spw <= 4 && lane_runner == 1)
+                hipLaunchKernelGGL((pll_spec_lane_kernel<kPllBatch, 1>), grid, block, runner_lds, s, x, m, n_streams, spw,
+                                   stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
+            else if (spw == 1 && lane_runner == 3)
+                hipLaunchKernelGGL((pll_spec_lane_kernel<kPllBatch, 2>), grid, block, runner_lds, s, x, m, n_streams, spw,
+                                   stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
+            else if (spw <= 4 && lane_runner == 2)
+                hipLaunchKernelGGL((pll_spec_lane_kernel<kPllBatch, 0>), grid, block, runner_lds, s, x, m, n_streams, spw,
+                                   stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
+            else if (spw <= 4)
+                hipLaunchKernelGGL((pll_spec_kernel<kPllBatch, true>), grid, block, runner_lds, s, x, m, n_streams, spw,
                                    stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
             else
-                hipLaunchKernelGGL((pll_spec_kernel<kPllBatch, false>), grid, block, 0, s, x, m, n_streams, spw,
+                hipLaunchKernelGGL((pll_spec_kernel<kPllBatch, false>), grid, block, runner_lds, s, x, m, n_streams, spw,
                                    stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
             const int nb = m / kPllBatch;
             if (nb > 0)
