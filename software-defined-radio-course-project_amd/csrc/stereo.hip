@@ -471,6 +471,10 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
         ld_d(pr, spr, 1, q);
         ld_d(hz, shl, 1, q);
     }
+    // land batch 1 before the loop: the loop's back edge then carries the only loads in flight
+    // at its top (a load issued last here would otherwise make every batch start with a full
+    // wait, the waitcnt pass merging both edges)
+    __builtin_amdgcn_s_waitcnt(0);
     // the state of batch 1's first step, as pll_batch_fast starts (every lane alike)
     const int q0 = ctx.q;
     const float u0 = (q0 & 1) ? p.fbQ : p.fbI, w0 = (q0 & 1) ? p.fbI : -p.fbQ;
@@ -528,14 +532,15 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
             // would overlap the old values and cost a register copy per element a batch
             __builtin_amdgcn_sched_barrier(0);
         }
-        if (inject >= 0 && b == 1 + (inject + s) % (nb - 1)) phase += 1.0e-3f;  // test hook: a wrong batch
-        if (owner) {
-            float* ob = out + b * NB;
+        // test hook (a wrong batch), branch-free
+        phase += (inject >= 0 && b == 1 + (inject + s) % (nb - 1)) ? 1.0e-3f : 0.0f;
+        // every lane stores: the lanes of a row hold the same values, and rows past the last
+        // stream recompute it bit for bit, so the writes agree; with no branch around them
+        // the loads in flight across the loop's back edge need no full wait at its top
+        float* ob = out + b * NB;
 #pragma unroll
-            for (int q = 0; q < NB / 4; q++)
-                reinterpret_cast<float4*>(ob)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
-            rec[(size_t)s * rb + b] = make_float2(integ, phase);
-        }
+        for (int q = 0; q < NB / 4; q++) reinterpret_cast<float4*>(ob)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
+        rec[(size_t)s * rb + b] = make_float2(integ, phase);
     }
 }
 
