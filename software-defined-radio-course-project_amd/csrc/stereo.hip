@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(256) pll_prep_kernel(const float* io, int m, i
 }
 
 // The same side data stream-major (element (j, s) at s seg + j: each stream's samples
-// contiguous), for the split kernels: a wave there works on at most 4 streams, so stream-minor
+// contiguous; the half turns with zero gaps, 2 seg per stream), for the split kernels: a wave there works on at most 4 streams, so stream-minor
 // rows would put every 16-B load of a wave on its own page (rows n_streams x 16 B apart).
 // One thread per sample pair.
 __global__ void __launch_bounds__(256) pll_prep_major_kernel(const float* io, int m, int n_streams, size_t stride,
@@ -159,7 +159,11 @@ __global__ void __launch_bounds__(256) pll_prep_major_kernel(const float* io, in
     const size_t plane = seg * (size_t)n_streams / 2, a = (size_t)s * (seg / 2) + jp;
     siv[a] = iv;
     siv[plane + a] = pr;
-    siv[2 * plane + a] = h;
+    // half turns in 32-B groups (h_2jp, h_2jp+1, 0, 0): pll_spec_lane_kernel's lane 2 reads the
+    // first 16 B, the row's other lanes the zeros beside them (same cache line, no mask op)
+    double2* sh = siv + 2 * plane + (size_t)s * seg + 2 * (size_t)jp;
+    sh[0] = h;
+    sh[1] = make_double2(0.0, 0.0);
 }
 
 // n exact steps (pll_step with the library fallbacks), out of line: the kernel then holds no
@@ -321,16 +325,15 @@ __global__ void __launch_bounds__(256) pll_kernel(float* io, int n, int n_stream
 // induction every batch before fail[s] is exact.  pll_kernel (with `fail`) resumes from there
 // on the certified path and runs the tail, so the result equals the plain launch bit for bit
 // whatever the runner did; when everything verified it only runs the tail.
-template <int NB, bool SPLIT>
+template <int NB>
 __global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, int n_streams, int spw, size_t stride,
                                                       const double* side, size_t seg, double step, float norm_bw,
                                                       const float* st, float* out_base, size_t ostride, int* fail,
                                                       float2* rec, size_t rb, int inject) {
     const int t = threadIdx.x & 63;
     const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int s_lane = wave * spw + (SPLIT ? ((t >> 4) & (spw - 1)) : (t & (spw - 1)));
-    const bool owner = (SPLIT ? ((t & 15) == 0 && (t >> 4) < spw) : t < spw) && s_lane < n_streams;
-    const SplitCoef sc = split_coef((t & 1) != 0);
+    const int s_lane = wave * spw + (t & (spw - 1));
+    const bool owner = t < spw && s_lane < n_streams;
     const int s = s_lane < n_streams ? s_lane : n_streams - 1;
     const float* x = io + (size_t)s * stride;
     float* out = out_base + (size_t)s * ostride;
@@ -359,8 +362,7 @@ __global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, i
         *reinterpret_cast<float4*>(&v[4 * q]) = reinterpret_cast<const float4*>(x + b * NB)[q];
     };
     auto ld_d = [&](double (&dst)[NB], const double2* row, int b, int q) {
-        *reinterpret_cast<double2*>(&dst[2 * q]) = SPLIT ? row[(size_t)s * (seg / 2) + b * (NB / 2) + q]
-                                                        : (row + (size_t)(b * (NB / 2) + q) * n_streams)[s];
+        *reinterpret_cast<double2*>(&dst[2 * q]) = (row + (size_t)(b * (NB / 2) + q) * n_streams)[s];
     };
     if (nb > 1) {
 #pragma unroll
@@ -384,7 +386,7 @@ __global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, i
             __builtin_amdgcn_sched_barrier(0);  // see pll_spec_lane_kernel
         };
         float o[NB];
-        (void)pll_batch_fast<NB, SPLIT, true>(p, ctx, v, iv, pr, o, Ki, Kp, refill, sc, hh);
+        (void)pll_batch_fast<NB, false, true>(p, ctx, v, iv, pr, o, Ki, Kp, refill, SplitCoef{}, hh);
         if (inject >= 0 && b == 1 + (inject + s) % (nb - 1)) p.phase += 1.0e-3f;  // test hook: a wrong batch
         if (owner) {
             float* ob = out + b * NB;
@@ -396,10 +398,11 @@ __global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, i
     }
 }
 
-// ---- the speculative runner with lane roles (split layout, 16-lane rows) ---------------------
+// ---- the speculative runner with lane roles (split layout, 16-lane rows; spw <= 4) ------------
 //
-// pll_spec_kernel<SPLIT> already evaluates sin and cos as one polynomial on even / odd lanes.
-// This form gives a third lane of each row a job too: the two reductions of a step's trigArg
+// pll_spec_kernel's recurrence with the lanes of a row (one stream) doing different work:
+// sin and cos are one polynomial on even / odd lanes (pll_sincos_split), and lane 2 takes a
+// third job.  The two reductions of a step's trigArg
 // x -- r = x - nd pi/2 for sin/cos and the atan2 offset B = (m - h) 2 pi - x of the NEXT step
 // (pll_offset_h) -- are the same five operations with different constants,
 //     t = rint(fma(x, C1, H)) - H,   w = fma(-t, Clo, fma(-t, Chi, x)),
@@ -407,17 +410,18 @@ __global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, i
 // fma(x, C1, +0) is the rounded product) and (1/(2 pi), 2 pi hi, 2 pi lo, half turn) on lane 2
 // of the row (w = -B, bit for bit: fma is odd under negating an operand pair), so lane 2
 // computes the offset while the others compute r, and a third row broadcast hands -B to every
-// lane.  Every lane loads its stream's half turns; a per-lane mask zeroes them off lane 2.
+// lane.  The half turns reach lane 2 only: the other lanes load the zeros stored beside them.
 // The batch state (fc, nfs, sn, cs, -B) stays in registers from batch to batch; nothing on
 // the serial chain is a packed op (a packed f32 result read by the next instruction costs a
-// wait state on gfx950).  The result is checked by pll_check_kernel like pll_spec_kernel's.
+// wait state on gfx950).  ~36 VALU a step, 82 % of the wave's cycles issuing VALU
+// (profiles/r02/runner/).  The result is checked by pll_check_kernel like pll_spec_kernel's.
 template <int L>
 __device__ inline double row_bcast(double v) {
     const long long bits = __builtin_bit_cast(long long, v);
     return __builtin_bit_cast(double, (long long)__builtin_amdgcn_mov_dpp(bits, 0x150 + L, 0xF, 0xF, false));
 }
 
-template <int NB, int LB>
+template <int NB>
 __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int n, int n_streams, int spw,
                                                            size_t stride, const double* side, size_t seg, double step,
                                                            float norm_bw, const float* st, float* out_base,
@@ -437,9 +441,8 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
     float* out = out_base + (size_t)s * ostride;
     const double2* siv = reinterpret_cast<const double2*>(side) + (size_t)s * (seg / 2);
     const double2* spr = reinterpret_cast<const double2*>(side) + seg * (size_t)n_streams / 2 + (size_t)s * (seg / 2);
-    const double2* shl = reinterpret_cast<const double2*>(side) + seg * (size_t)n_streams + (size_t)s * (seg / 2);
-    // the half turn's high dword survives on lane 2 only (its low dword is 0 for 0.5 and 0)
-    const uint64_t hmask = ((uint64_t)(b_lane ? 0xFFFFFFFFu : 0u) << 32) | 0xFFFFFFFFull;
+    // half turns: lane 2 reads (h_j, h_j+1), the other lanes the zero pair beside it
+    const double2* shl = reinterpret_cast<const double2*>(side) + seg * (size_t)n_streams + (size_t)s * seg + (b_lane ? 0 : 1);
     const float* S = st + 8 * (size_t)s;
     const float Kp = norm_bw * static_cast<float>(2.666);
     const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
@@ -463,13 +466,16 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
     auto ld_d = [&](double (&dst)[NB], const double2* row, int b, int q) {
         *reinterpret_cast<double2*>(&dst[2 * q]) = row[b * (NB / 2) + q];
     };
+    auto ld_h = [&](int b, int q) {
+        *reinterpret_cast<double2*>(&hz[2 * q]) = shl[2 * (b * (NB / 2) + q)];
+    };
 #pragma unroll
     for (int q = 0; q < NB / 4; q++) ld_v(1, q);
 #pragma unroll
     for (int q = 0; q < NB / 2; q++) {
         ld_d(iv, siv, 1, q);
         ld_d(pr, spr, 1, q);
-        ld_d(hz, shl, 1, q);
+        ld_h(1, q);
     }
     // land batch 1 before the loop: the loop's back edge then carries the only loads in flight
     // at its top (a load issued last here would otherwise make every batch start with a full
@@ -498,23 +504,10 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
             const float arg = (float)(pr[j] + (double)phase);
             o[j] = arg;
             const double xa = (double)arg;
-            double w;
-            if constexpr (LB != 0) {
-                const double H = __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, hz[(j + 1) % NB]) & hmask);
-                const double tq = rint(fma(xa, C1, H)) - H;
-                w = fma(-tq, Clo, fma(-tq, Chi, xa));  // r, or -B on lane 2
-                if constexpr (LB == 1) {
-                    nB = row_bcast<2>(w);
-                } else {  // one stream per wave: lane 2's value through two SGPRs
-                    const long long wb = __builtin_bit_cast(long long, w);
-                    const int lo = __builtin_amdgcn_readlane((int)wb, 2), hi = __builtin_amdgcn_readlane((int)(wb >> 32), 2);
-                    nB = __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-                }
-            } else {
-                const double nd = rint(xa * kInvPio2);
-                w = fma(-nd, kPio2Lo, fma(-nd, kPio2Hi, xa));
-                nB = -pll_offset_h(xa, hz[(j + 1) % NB]);
-            }
+            const double H = hz[(j + 1) % NB];  // the next step's half turn on lane 2, else 0
+            const double tq = rint(fma(xa, C1, H)) - H;
+            const double w = fma(-tq, Clo, fma(-tq, Chi, xa));  // r, or -B on lane 2
+            nB = row_bcast<2>(w);
             const double z = w * w;
             const double W = split_w_horner(z, sc);
             sn = row_bcast<0>(w * W);
@@ -526,7 +519,7 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
             if (j % 2 == 1) {
                 ld_d(iv, siv, bn, j / 2);
                 ld_d(pr, spr, bn, j / 2);
-                ld_d(hz, shl, bn, j / 2);
+                ld_h(bn, j / 2);
             }
             // keep each refill after the step that consumed its registers: hoisted loads
             // would overlap the old values and cost a register copy per element a batch
@@ -865,7 +858,7 @@ static size_t pll_seg_len(int n, int n_streams) {
 }
 size_t pll_side_doubles(int n, int n_streams) {
     const size_t seg = pll_seg_len(n, n_streams);
-    return (3 * seg + seg / 2 + seg / kPllBatch) * (size_t)n_streams + ((size_t)n_streams + 1) / 2;
+    return (4 * seg + seg / 2 + seg / kPllBatch) * (size_t)n_streams + ((size_t)n_streams + 1) / 2;
 }
 
 // The recurrence in segments of at most kPllSeg samples per stream: side data of the segment
@@ -879,7 +872,7 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     if (n <= 0) return 0;
     const size_t seg = pll_seg_len(n, n_streams);
     const size_t rb = seg / kPllBatch;
-    float* args = reinterpret_cast<float*>(side + 3 * seg * (size_t)n_streams);  // seg per stream
+    float* args = reinterpret_cast<float*>(side + 4 * seg * (size_t)n_streams);  // seg per stream
     float2* rec = reinterpret_cast<float2*>(args + seg * (size_t)n_streams);      // rb per stream
     int* fail = reinterpret_cast<int*>(rec + rb * (size_t)n_streams);
     // one stream per wave while the waves fit one per SIMD, then more streams per wave
@@ -899,11 +892,6 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         return e ? std::atoi(e) : -1;
     }();
     const bool spec = spec_env && (reinterpret_cast<uintptr_t>(io) & 15) == 0 && stride % 4 == 0;
-    // FMRX_PLL_RUNNER=0: the runner without lane roles (A/B measurements)
-    const int lane_runner = [] {  // 1 lane roles (default), 2 the same without the offset lane
-        const char* e = std::getenv("FMRX_PLL_RUNNER");
-        return e ? std::atoi(e) : 1;
-    }();
     int spw = 1;
     while (spw < 64 && (long long)spw * n_simd < n_streams) spw *= 2;
     // Waves of 64 lanes; past 256 waves, workgroups of 4 waves, one per SIMD of a CU: 64-lane
@@ -911,11 +899,7 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     const int waves = (n_streams + spw - 1) / spw;
     const int wpg = waves > n_simd / 4 ? 4 : 1;
     const dim3 grid((waves + wpg - 1) / wpg), block(64 * wpg);
-    // FMRX_PLL_LDS (bytes, experiments): dynamic LDS per runner workgroup, to pin one per CU
-    static const unsigned runner_lds = [] {
-        const char* e = std::getenv("FMRX_PLL_LDS");
-        return e ? (unsigned)std::atoi(e) : 0u;
-    }();
+
     // filter.cpp:163: 2*PI*(freq/Fs) in double from the float quotient (host == device IEEE)
     const double step = (2.0 * 3.14159265358979323846) * static_cast<double>(freq / fs);  // dy4.h:14 PI
     for (size_t off = 0; off < (size_t)n; off += seg) {
@@ -930,20 +914,11 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         float* out = spec ? args : x;
         const size_t ostride = spec ? seg : stride;
         if (spec) {
-            if (spw <= 4 && lane_runner == 1)
-                hipLaunchKernelGGL((pll_spec_lane_kernel<kPllBatch, 1>), grid, block, runner_lds, s, x, m, n_streams, spw,
-                                   stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
-            else if (spw == 1 && lane_runner == 3)
-                hipLaunchKernelGGL((pll_spec_lane_kernel<kPllBatch, 2>), grid, block, runner_lds, s, x, m, n_streams, spw,
-                                   stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
-            else if (spw <= 4 && lane_runner == 2)
-                hipLaunchKernelGGL((pll_spec_lane_kernel<kPllBatch, 0>), grid, block, runner_lds, s, x, m, n_streams, spw,
-                                   stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
-            else if (spw <= 4)
-                hipLaunchKernelGGL((pll_spec_kernel<kPllBatch, true>), grid, block, runner_lds, s, x, m, n_streams, spw,
-                                   stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
+            if (spw <= 4)
+                hipLaunchKernelGGL(pll_spec_lane_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw, stride,
+                                   side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
             else
-                hipLaunchKernelGGL((pll_spec_kernel<kPllBatch, false>), grid, block, runner_lds, s, x, m, n_streams, spw,
+                hipLaunchKernelGGL(pll_spec_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw,
                                    stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
             const int nb = m / kPllBatch;
             if (nb > 0)
