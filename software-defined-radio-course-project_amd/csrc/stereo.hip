@@ -412,8 +412,8 @@ __global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, i
 // computes the offset while the others compute r, and a third row broadcast hands -B to every
 // lane.  The half turns reach lane 2 only: the other lanes load the zeros stored beside them.
 // The batch state (fc, nfs, sn, cs, -B) stays in registers from batch to batch; nothing on
-// the serial chain is a packed op (a packed f32 result read by the next instruction costs a
-// wait state on gfx950).  ~36 VALU a step, 82 % of the wave's cycles issuing VALU
+// the serial chain is a packed op but the first product (a packed f32 result read by the next
+// instruction costs a wait state on gfx950).  ~36 VALU a step, 82 % of the wave's cycles issuing VALU
 // (profiles/r02/runner/).  The result is checked by pll_check_kernel like pll_spec_kernel's.
 template <int L>
 __device__ inline double row_bcast(double v) {
@@ -493,8 +493,10 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
         float o[NB];
 #pragma unroll
         for (int j = 0; j < NB; j++) {
-            const float a = v[j] * fc;
-            const float bb = v[j] * nfs;
+            // the one packed op on the chain: one instruction for both products, its wait state
+            // often filled by scalar work (measured 0.4 % faster than two v_mul_f32)
+            const float2v ab = float2v{fc, nfs} * v[j];
+            const float a = ab.x, bb = ab.y;
             const double Y = fma((double)a, sn, (double)bb * cs);
             const float e = (float)fma(Y, iv[j], -nB);
             const float ki_e = Ki * e;

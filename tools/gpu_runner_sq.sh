@@ -1,14 +1,17 @@
 #!/bin/bash
-# SQ + GRBM counter passes of the speculative PLL runner at 1 and 1,024 streams, both runner
-# forms (FMRX_PLL_RUNNER=1 lane roles, 0 the previous one): issue, waits and the clock.
+# SQ + GRBM counter passes of the speculative PLL runner at 1 and 1,024 streams, runner forms
+# given by FMRX_PLL_RUNNER values (default "1 0": lane roles, the previous form).
 set -o pipefail
 OUT=gpurun_out/${1:-runner_sq}
+RUNNERS=${2:-"1 0"}
+STREAMS=${3:-"1 1024"}
 mkdir -p $OUT
 export TMPDIR=/tmp
 i=0
-for ns in 1 1024; do
-  for r in 1 0; do
+for ns in $STREAMS; do
+  for r in $RUNNERS; do
     for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
+               "SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_VALU SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH" \
                "GRBM_GUI_ACTIVE GRBM_COUNT"; do
       i=$((i+1))
       echo "pass $i ns=$ns runner=$r $grp" >> $OUT/passes.txt
