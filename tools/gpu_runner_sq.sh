@@ -14,8 +14,8 @@ for ns in $STREAMS; do
                "SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_VALU SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH" \
                "GRBM_GUI_ACTIVE GRBM_COUNT"; do
       i=$((i+1))
-      echo "pass $i ns=$ns runner=$r $grp" >> $OUT/passes.txt
-      FMRX_PLL_RUNNER=$r timeout -k 10 -s KILL 120 rocprofv3 --pmc $grp -T -d $OUT/p$i -o run --output-format csv -- \
+      echo "pass $i ns=$ns runner $grp" >> $OUT/passes.txt
+      timeout -k 10 -s KILL 120 rocprofv3 --pmc $grp -T -d $OUT/p$i -o run --output-format csv -- \
           python3 tools/bench_stereo.py --streams $ns --seconds 4 > $OUT/p$i.log 2>&1 || { echo "pass $i failed" >> $OUT/failed.txt; exit 1; }
     done
   done
