@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "dsp_device.h"
 #include "fmrx_internal.h"
@@ -172,11 +173,17 @@ struct PllPair {
     PllState p;
     PllCtx ctx;
 };
+// `wr` false: compute only.  Lanes of the grid's padding waves (s_lane >= n_streams) recompute
+// the last stream but do not run in lockstep with its own wave, which in the plain launch
+// overwrites the input in place: they must not write what they derived from it.
 __device__ __noinline__ PllPair pll_redo(PllState p, PllCtx ctx, const float* xb, float* ob, int n, float Ki,
-                                         float Kp, double step) {
+                                         float Kp, double step, bool wr) {
     const DeviceLib lib;
 #pragma unroll 1
-    for (int j = 0; j < n; j++) ob[j] = pll_step(p, ctx, xb[j], Ki, Kp, step, lib);
+    for (int j = 0; j < n; j++) {
+        const float a = pll_step(p, ctx, xb[j], Ki, Kp, step, lib);
+        if (wr) ob[j] = a;
+    }
     return PllPair{p, ctx};
 }
 
@@ -295,9 +302,9 @@ __global__ void __launch_bounds__(256) pll_kernel(float* io, int n, int n_stream
                     for (int q = 0; q < NB / 4; q++)
                         reinterpret_cast<float4*>(ob)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
                 }
-            } else {  // rare: redo from the saved state on the exact path (duplicate lanes of the
-                      // last stream read and write its samples in lockstep, identical values)
-                const PllPair r = pll_redo(p0, ctx0, xb, ob, NB, Ki, Kp, step);
+            } else {  // rare: redo from the saved state on the exact path (duplicate rows of a
+                      // wave write in lockstep, identical values; padding waves do not write)
+                const PllPair r = pll_redo(p0, ctx0, xb, ob, NB, Ki, Kp, step, s_lane < n_streams);
                 p = r.p;
                 ctx = r.ctx;
             }
@@ -305,7 +312,7 @@ __global__ void __launch_bounds__(256) pll_kernel(float* io, int n, int n_stream
         i = nb * NB;
     }
     if (i < n) {  // tail (and unaligned streams): exact steps
-        const PllPair r = pll_redo(p, ctx, x + i, out + i, n - i, Ki, Kp, step);
+        const PllPair r = pll_redo(p, ctx, x + i, out + i, n - i, Ki, Kp, step, s_lane < n_streams);
         p = r.p;
     }
     if (owner) {
@@ -351,7 +358,7 @@ __global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, i
     PllCtx ctx{};
     ctx.valid = false;
     if (nb > 0) {
-        const PllPair r = pll_redo(p, ctx, x, out, NB, Ki, Kp, step);
+        const PllPair r = pll_redo(p, ctx, x, out, NB, Ki, Kp, step, s_lane < n_streams);
         p = r.p;
         ctx = r.ctx;
         if (owner) rec[(size_t)s * rb] = make_float2(p.integ, p.phase);
@@ -426,7 +433,7 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
                                                            size_t stride, const double* side, size_t seg, double step,
                                                            float norm_bw, const float* st, float* out_base,
                                                            size_t ostride, int* fail, float2* rec, size_t rb,
-                                                           int inject) {
+                                                           int inject, int sat_ok) {
     const int t = threadIdx.x & 63;
     const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int s_lane = wave * spw + ((t >> 4) & (spw - 1));
@@ -452,7 +459,7 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
     PllCtx ctx{};
     ctx.valid = false;
     if (nb > 0) {  // batch 0 on the exact path (see pll_spec_kernel)
-        const PllPair r = pll_redo(p, ctx, x, out, NB, Ki, Kp, step);
+        const PllPair r = pll_redo(p, ctx, x, out, NB, Ki, Kp, step, s_lane < n_streams);
         p = r.p;
         ctx = r.ctx;
         if (owner) rec[(size_t)s * rb] = make_float2(p.integ, p.phase);
@@ -488,55 +495,96 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
     double sn = ctx.sn, cs = ctx.cs;
     double nB = -pll_offset_h(ctx.x, iv[0] < 0.0 ? 0.5 : 0.0);
     float integ = p.integ, phase = p.phase;
-    for (int b = 1; b < nb; b++) {
-        const int bn = b + 1 < nb ? b + 1 : b;
-        float o[NB];
+    // SAT: the segment starts with trigOffset stuck at 2^24 (filter.cpp:165-166 in float, from
+    // 69.9 s of signal on; pll_side), so trigArg = float(step 2^24 + phase) moves only when
+    // the phase crosses its 0.5 grid -- on ~7.5 % of steps (measured on the bench stream).  With
+    // one stream per wave the test is wave-uniform: a scalar branch skips the sin/cos polynomial,
+    // its broadcasts and conversions (same bits in, same bits out).  The reduction still runs
+    // every step: lane 2's offset B also depends on the next sample's half turn.
+    // the rotation's Y = a sn + b cs of a sample from the current feedback (fc, nfs, sn, cs); the
+    // one packed op on the chain: one instruction for both products, its wait state often filled
+    // by scalar work (measured 0.4 % faster than two v_mul_f32)
+    auto y_of = [&](float vv) -> double {
+        const float2v ab = float2v{fc, nfs} * vv;
+        return fma((double)ab.x, sn, (double)ab.y * cs);
+    };
+    auto run = [&](auto sat_tag) {
+        constexpr bool SAT = decltype(sat_tag)::value;
+        uint32_t prev = __builtin_bit_cast(uint32_t, (float)ctx.x);  // the trigArg sn, cs belong to
+        // SAT: the next step's Y is formed before the branch on this step's repeat resolves (the
+        // branch waits for its compare; the common repeat keeps sn, cs, so Y stands), and again
+        // on the rare fresh path
+        double Yn = SAT ? y_of(v[0]) : 0.0;
+        for (int b = 1; b < nb; b++) {
+            const int bn = b + 1 < nb ? b + 1 : b;
+            float o[NB];
 #pragma unroll
-        for (int j = 0; j < NB; j++) {
-            // the one packed op on the chain: one instruction for both products, its wait state
-            // often filled by scalar work (measured 0.4 % faster than two v_mul_f32)
-            const float2v ab = float2v{fc, nfs} * v[j];
-            const float a = ab.x, bb = ab.y;
-            const double Y = fma((double)a, sn, (double)bb * cs);
-            const float e = (float)fma(Y, iv[j], -nB);
-            const float ki_e = Ki * e;
-            const float kp_e = Kp * e;
-            integ = integ + ki_e;
-            phase = phase + (kp_e + integ);
-            const float arg = (float)(pr[j] + (double)phase);
-            o[j] = arg;
-            const double xa = (double)arg;
-            const double H = hz[(j + 1) % NB];  // the next step's half turn on lane 2, else 0
-            const double tq = rint(fma(xa, C1, H)) - H;
-            const double w = fma(-tq, Clo, fma(-tq, Chi, xa));  // r, or -B on lane 2
-            nB = row_bcast<2>(w);
-            const double z = w * w;
-            const double W = split_w_horner(z, sc);
-            sn = row_bcast<0>(w * W);
-            cs = row_bcast<1>(W);
-            fc = (float)cs;
-            nfs = -(float)sn;
-            // refill after step j: v[j], iv[j], pr[j] and hz[j] (read at step j - 1) are dead
-            if (j % 4 == 3) ld_v(bn, j / 4);
-            if (j % 2 == 1) {
-                ld_d(iv, siv, bn, j / 2);
-                ld_d(pr, spr, bn, j / 2);
-                ld_h(bn, j / 2);
+            for (int j = 0; j < NB; j++) {
+                const double Y = SAT ? Yn : y_of(v[j]);
+                const float e = (float)fma(Y, iv[j], -nB);
+                const float ki_e = Ki * e;
+                const float kp_e = Kp * e;
+                integ = integ + ki_e;
+                phase = phase + (kp_e + integ);
+                const float arg = (float)(pr[j] + (double)phase);
+                o[j] = arg;
+                const double xa = (double)arg;
+                const double H = hz[(j + 1) % NB];  // the next step's half turn on lane 2, else 0
+                const double tq = rint(fma(xa, C1, H)) - H;
+                const double w = fma(-tq, Clo, fma(-tq, Chi, xa));  // r, or -B on lane 2
+                nB = row_bcast<2>(w);
+                auto sincos_step = [&] {
+                    const double z = w * w;
+                    const double W = split_w_horner(z, sc);
+                    sn = row_bcast<0>(w * W);
+                    cs = row_bcast<1>(W);
+                    fc = (float)cs;
+                    nfs = -(float)sn;
+                };
+                if constexpr (SAT) {
+                    const uint32_t ab_bits = __builtin_bit_cast(uint32_t, arg);
+                    const bool changed = __builtin_amdgcn_ballot_w64(ab_bits != prev) != 0;
+                    prev = ab_bits;
+                    // step j + 1's sample: for the last step, the next batch's first (refilled
+                    // at step 3)
+                    const float vn = v[(j + 1) % NB];
+                    Yn = y_of(vn);
+                    asm volatile("" : "+v"(Yn));  // formed here, not sunk past the branch
+                    // unlikely: laid out of line, so the common repeat falls through
+                    if (__builtin_expect(changed, 0)) {
+                        sincos_step();
+                        Yn = y_of(vn);
+                    }
+                } else {
+                    sincos_step();
+                }
+                // refill after step j: v[j], iv[j], pr[j] and hz[j] (read at step j - 1) are dead
+                if (j % 4 == 3) ld_v(bn, j / 4);
+                if (j % 2 == 1) {
+                    ld_d(iv, siv, bn, j / 2);
+                    ld_d(pr, spr, bn, j / 2);
+                    ld_h(bn, j / 2);
+                }
+                // keep each refill after the step that consumed its registers: hoisted loads
+                // would overlap the old values and cost a register copy per element a batch
+                __builtin_amdgcn_sched_barrier(0);
             }
-            // keep each refill after the step that consumed its registers: hoisted loads
-            // would overlap the old values and cost a register copy per element a batch
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // test hook (a wrong batch), branch-free
-        phase += (inject >= 0 && b == 1 + (inject + s) % (nb - 1)) ? 1.0e-3f : 0.0f;
-        // every lane stores: the lanes of a row hold the same values, and rows past the last
-        // stream recompute it bit for bit, so the writes agree; with no branch around them
-        // the loads in flight across the loop's back edge need no full wait at its top
-        float* ob = out + b * NB;
+            // test hook (a wrong batch), branch-free
+            phase += (inject >= 0 && b == 1 + (inject + s) % (nb - 1)) ? 1.0e-3f : 0.0f;
+            // every lane stores: the lanes of a row hold the same values, and rows past the last
+            // stream recompute it bit for bit, so the writes agree; with no branch around them
+            // the loads in flight across the loop's back edge need no full wait at its top
+            float* ob = out + b * NB;
 #pragma unroll
-        for (int q = 0; q < NB / 4; q++) reinterpret_cast<float4*>(ob)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
-        rec[(size_t)s * rb + b] = make_float2(integ, phase);
-    }
+            for (int q = 0; q < NB / 4; q++)
+                reinterpret_cast<float4*>(ob)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
+            rec[(size_t)s * rb + b] = make_float2(integ, phase);
+        }
+    };
+    if (sat_ok && spw == 1 && p.trig == kPllTrigStick)
+        run(std::true_type{});
+    else
+        run(std::false_type{});
 }
 
 // One thread per (batch, stream): NB exact steps from the recorded start, compared bit for
@@ -894,6 +942,11 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         return e ? std::atoi(e) : -1;
     }();
     const bool spec = spec_env && (reinterpret_cast<uintptr_t>(io) & 15) == 0 && stride % 4 == 0;
+    // FMRX_PLL_SAT=0 (measurements, tests): no sin/cos skipping once trigOffset has stuck at 2^24
+    const int sat_ok = [] {
+        const char* e = std::getenv("FMRX_PLL_SAT");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
     int spw = 1;
     while (spw < 64 && (long long)spw * n_simd < n_streams) spw *= 2;
     // Waves of 64 lanes; past 256 waves, workgroups of 4 waves, one per SIMD of a CU: 64-lane
@@ -918,7 +971,7 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         if (spec) {
             if (spw <= 4)
                 hipLaunchKernelGGL(pll_spec_lane_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw, stride,
-                                   side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
+                                   side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject, sat_ok);
             else
                 hipLaunchKernelGGL(pll_spec_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw,
                                    stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);

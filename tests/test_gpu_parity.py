@@ -479,6 +479,7 @@ def test_primitives(fmrx, taps_golden):
 @pytest.mark.parametrize("trig,phase,freq,fs,n,offset", [
     (0.0, 0.0, 19000, 240000, 4103, 0),              # n % 16 != 0: exact tail
     (16777200.0, 0.25, 19000, 240000, 700, 0),       # trigOffset sticks at 2^24 inside a batch
+    (16777216.0, 0.3, 19000, 240000, 6000, 0),       # stuck from the start: the runner's sin/cos skipping
     (0.5, 0.0, 19000, 240000, 300, 0),               # non-integer trigOffset: exact path only
     (3.0e7, 0.0, 19000, 240000, 300, 0),             # past 2^24: exact path only
     (0.0, 6.0e8, 19000, 240000, 300, 0),             # |phaseEst| beyond the batch's range check
@@ -502,6 +503,31 @@ def test_pll_primitive_states(fmrx, orc, trig, phase, freq, fs, n, offset):
         rx.pll(buf.data_ptr() + 4 * offset, n, freq, fs, 2.0, 0.0, 0.01, st.data_ptr())
         rx.synchronize()
         assert same(buf.cpu().numpy()[offset:], want_x)
+        assert same(st.cpu().numpy(), want_st)
+
+
+@pytest.mark.parametrize("inject", [None, "3"])
+@pytest.mark.parametrize("sat", ["1", "0"])
+def test_pll_saturated_runner(fmrx, orc, monkeypatch, inject, sat):
+    """A segment that starts with trigOffset stuck at 2^24 (filter.cpp:165-166 in float, 69.9 s
+    into a stream): the speculative runner skips the sin/cos of repeated trigArgs; with and
+    without that skipping, and with a corrupted runner batch (check + certified resume)."""
+    monkeypatch.setenv("FMRX_PLL_SAT", sat)
+    if inject is not None:
+        monkeypatch.setenv("FMRX_PLL_SPEC_INJECT", inject)
+    n = 20000
+    rng = np.random.default_rng(24)
+    t = np.arange(n)
+    x = (0.1 * np.cos(2 * np.pi * 19000 / 240000 * t + 0.3) + 0.01 * rng.standard_normal(n)).astype(np.float32)
+    st0 = np.array([2e-4, 1.7, 0.6, 0.8, 1.0, 16777216.0], np.float32)
+    want_x, want_st = orc.pll(x, 19000, 240000, 2.0, 0.0, 0.01, st0)
+    with fmrx.Receiver(0, fmrx.STEREO) as rx:
+        buf = _d(x)
+        st = _d(st0)
+        torch.cuda.synchronize()
+        rx.pll(buf.data_ptr(), n, 19000, 240000, 2.0, 0.0, 0.01, st.data_ptr())
+        rx.synchronize()
+        assert same(buf.cpu().numpy(), want_x)
         assert same(st.cpu().numpy(), want_st)
 
 
