@@ -440,16 +440,11 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
     const bool owner = (t & 15) == 0 && (t >> 4) < spw && s_lane < n_streams;
     const bool b_lane = (t & 15) == 2;
     const SplitCoef sc = split_coef((t & 1) != 0);
-    const double C1 = b_lane ? kInv2Pi : kInvPio2;
-    const double Chi = b_lane ? k2PiHi : kPio2Hi;
-    const double Clo = b_lane ? k2PiLo : kPio2Lo;
     const int s = s_lane < n_streams ? s_lane : n_streams - 1;
     const float* x = io + (size_t)s * stride;
     float* out = out_base + (size_t)s * ostride;
     const double2* siv = reinterpret_cast<const double2*>(side) + (size_t)s * (seg / 2);
     const double2* spr = reinterpret_cast<const double2*>(side) + seg * (size_t)n_streams / 2 + (size_t)s * (seg / 2);
-    // half turns: lane 2 reads (h_j, h_j+1), the other lanes the zero pair beside it
-    const double2* shl = reinterpret_cast<const double2*>(side) + seg * (size_t)n_streams + (size_t)s * seg + (b_lane ? 0 : 1);
     const float* S = st + 8 * (size_t)s;
     const float Kp = norm_bw * static_cast<float>(2.666);
     const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
@@ -465,6 +460,18 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
         if (owner) rec[(size_t)s * rb] = make_float2(p.integ, p.phase);
     }
     if (nb < 2) return;
+    // SAT (trigOffset stuck at 2^24 for the whole segment, one stream a wave; see run below)
+    const bool sat = sat_ok && spw == 1 && p.trig == kPllTrigStick;
+    // reduction constants: 2 pi on the offset lanes (lane 2; with SAT lane 3 too), pi/2 on the
+    // sin/cos lanes
+    const bool two_pi = b_lane || (sat && (t & 15) == 3);
+    const double C1 = two_pi ? kInv2Pi : kInvPio2;
+    const double Chi = two_pi ? k2PiHi : kPio2Hi;
+    const double Clo = two_pi ? k2PiLo : kPio2Lo;
+    // half turns: lane 2 reads (h_j, h_j+1), the other lanes the zero pair beside it; with SAT
+    // every lane reads the values (the offset lanes' H is then a constant, see run)
+    const double2* shl =
+        reinterpret_cast<const double2*>(side) + seg * (size_t)n_streams + (size_t)s * seg + ((b_lane || sat) ? 0 : 1);
     float v[NB];
     double iv[NB], pr[NB], hz[NB];
     auto ld_v = [&](int b, int q) {
@@ -511,10 +518,18 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
     auto run = [&](auto sat_tag) {
         constexpr bool SAT = decltype(sat_tag)::value;
         uint32_t prev = __builtin_bit_cast(uint32_t, (float)ctx.x);  // the trigArg sn, cs belong to
-        // SAT: the next step's Y is formed before the branch on this step's repeat resolves (the
-        // branch waits for its compare; the common repeat keeps sn, cs, so Y stands), and again
-        // on the rare fresh path
-        double Yn = SAT ? y_of(v[0]) : 0.0;
+        // SAT: the offset of the next step depends on x and on that step's half turn only, so
+        // for a repeated trigArg it is one of two values, -B(x, 0) and -B(x, 1/2), refreshed
+        // with sin/cos (lanes 3 and 2, half turns as lane constants) and selected per step.
+        // The next step's Y is formed before the branch on this step's repeat resolves (the
+        // common repeat keeps sn, cs, so Y stands), and again on the rare fresh path.
+        double Yn = 0.0, nB0 = 0.0, nB1 = 0.0;
+        if constexpr (SAT) {
+            Yn = y_of(v[0]);
+            nB0 = -pll_offset_h(ctx.x, 0.0);
+            nB1 = -pll_offset_h(ctx.x, 0.5);
+        }
+        const double Hc = b_lane ? 0.5 : 0.0;  // SAT: lane 2 -B(x, 1/2), lane 3 -B(x, 0)
         for (int b = 1; b < nb; b++) {
             const int bn = b + 1 < nb ? b + 1 : b;
             float o[NB];
@@ -528,12 +543,8 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
                 phase = phase + (kp_e + integ);
                 const float arg = (float)(pr[j] + (double)phase);
                 o[j] = arg;
-                const double xa = (double)arg;
-                const double H = hz[(j + 1) % NB];  // the next step's half turn on lane 2, else 0
-                const double tq = rint(fma(xa, C1, H)) - H;
-                const double w = fma(-tq, Clo, fma(-tq, Chi, xa));  // r, or -B on lane 2
-                nB = row_bcast<2>(w);
-                auto sincos_step = [&] {
+                // sin/cos of r on the sin/cos lanes from the reduction's w
+                auto sincos_step = [&](double w) {
                     const double z = w * w;
                     const double W = split_w_horner(z, sc);
                     sn = row_bcast<0>(w * W);
@@ -552,11 +563,31 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
                     asm volatile("" : "+v"(Yn));  // formed here, not sunk past the branch
                     // unlikely: laid out of line, so the common repeat falls through
                     if (__builtin_expect(changed, 0)) {
-                        sincos_step();
+                        const double xa = (double)arg;
+                        const double tq = rint(fma(xa, C1, Hc)) - Hc;
+                        const double w = fma(-tq, Clo, fma(-tq, Chi, xa));  // r; -B(x, h) on lanes 2, 3
+                        nB1 = row_bcast<2>(w);
+                        nB0 = row_bcast<3>(w);
+                        sincos_step(w);
                         Yn = y_of(vn);
                     }
+                    // select by the half turn's bit 29 (set in 0.5's high dword, clear in 0):
+                    // one v_bfe_i32 and two v_bfi_b32, no compare-to-mask wait
+                    const uint64_t hb = __builtin_bit_cast(uint64_t, hz[(j + 1) % NB]);
+                    const uint32_t hi = (uint32_t)(hb >> 32);
+                    // the low dword is unused but still written by its load: keep it live here, or
+                    // the register allocator reuses it and the reuse waits for the load (vmcnt 0)
+                    asm volatile("" ::"v"((uint32_t)hb));
+                    const uint64_t m = (uint64_t)(uint32_t)__builtin_amdgcn_sbfe((int)hi, 29u, 1u) * 0x100000001ull;
+                    nB = __builtin_bit_cast(double, (m & __builtin_bit_cast(uint64_t, nB1)) |
+                                                        (~m & __builtin_bit_cast(uint64_t, nB0)));
                 } else {
-                    sincos_step();
+                    const double xa = (double)arg;
+                    const double H = hz[(j + 1) % NB];  // the next step's half turn on lane 2, else 0
+                    const double tq = rint(fma(xa, C1, H)) - H;
+                    const double w = fma(-tq, Clo, fma(-tq, Chi, xa));  // r, or -B on lane 2
+                    nB = row_bcast<2>(w);
+                    sincos_step(w);
                 }
                 // refill after step j: v[j], iv[j], pr[j] and hz[j] (read at step j - 1) are dead
                 if (j % 4 == 3) ld_v(bn, j / 4);
@@ -581,7 +612,7 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
             rec[(size_t)s * rb + b] = make_float2(integ, phase);
         }
     };
-    if (sat_ok && spw == 1 && p.trig == kPllTrigStick)
+    if (sat)
         run(std::true_type{});
     else
         run(std::false_type{});
