@@ -26,8 +26,7 @@ namespace {
 constexpr int kBpMax = 64;
 
 struct BpTaps {
-    float ch[kBpMax];
-    float ca[kBpMax];
+    float2 c[kBpMax];  // (channel, carrier) tap k, interleaved: one SGPR pair per packed product
 };
 
 // Channel (22-54 kHz) and carrier (18.5-19.5 kHz) band-pass FIRs share their input, so they
@@ -43,11 +42,69 @@ __global__ void __launch_bounds__(256) bpf_pair_kernel(StereoLaunch L, BpTaps t)
 #pragma unroll
     for (int k = 0; k < BT; k++) {
         const float xv = x[-k];
-        const float2v p = float2v{t.ch[k], t.ca[k]} * xv;
+        const float2v p = float2v{t.c[k].x, t.c[k].y} * xv;
         acc = acc + p;
     }
     L.channel[(size_t)s * L.n_if + j] = acc.x;
     L.carrier[(size_t)s * L.n_if + j] = acc.y;
+}
+
+// The same FIR pair tiled through LDS: a workgroup stages kBpTile outputs' demod samples plus
+// BT-1 of history once (coalesced), each thread keeps the window of its kBpR consecutive
+// outputs in registers (one ds_read_b128 per 4 samples, lane stride 16 B: conflict-free) and
+// the interleaved (h_ch, h_ca) taps are kernel arguments (SGPR pairs in the packed products).  Each output is
+// still the ascending-k sequential sum of separately rounded products (filter.cpp:84-92).
+// Replaces one global load per tap per output (51 VMEM instructions an output): 19.4 -> 15.1
+// ms per call at 1,024 streams x 10 s.  Measured and dropped: workgroups walking 8 tiles with
+// the next tile's loads in flight, and 8 outputs a thread (the taps then spill from SGPRs).
+constexpr int kBpR = 4, kBpThreads = 256, kBpTile = kBpR * kBpThreads;  // (the pin below names 4)
+template <int BT>
+__global__ void __launch_bounds__(kBpThreads) bpf_pair_tile_kernel(StereoLaunch L, BpTaps t) {
+    constexpr int W = kBpR + BT - 1;  // a thread's window: samples 4 tid .. 4 tid + W - 1 of the tile
+    constexpr int WV = (W + 1) / 2;   // float4 reads (two duplicated samples each)
+    // xs2[i] = (x, x), x = demod sample j0 - (BT - 1) + i: the packed product (h_ch, h_ca) * (x, x)
+    // needs no splat; the L.hist >= BT - 1 history samples sit in front of the call's demod
+    __shared__ float4 xs4[(kBpTile + BT - 1 + 1) / 2 + WV];
+    float2* xs2 = reinterpret_cast<float2*>(xs4);
+    const int s = blockIdx.y, tid = threadIdx.x;
+    const long long j0 = (long long)blockIdx.x * kBpTile;
+    const float* x = L.demod + (size_t)s * L.demod_stride + L.hist + j0 - (BT - 1);
+    const long long avail = (long long)L.n_if - j0 + (BT - 1);  // samples of this stream from x on
+    for (int i = tid; i < kBpTile + BT - 1; i += kBpThreads) {
+        const float v = i < avail ? x[i] : 0.0f;
+        xs2[i] = make_float2(v, v);
+    }
+    __syncthreads();
+    float2v win[2 * WV];
+#pragma unroll
+    for (int q = 0; q < WV; q++) {  // lane stride 32 B
+        const float4 w = xs4[2 * tid + q];
+        win[2 * q] = float2v{w.x, w.y};
+        win[2 * q + 1] = float2v{w.z, w.w};
+    }
+    float2v acc[kBpR];
+#pragma unroll
+    for (int r = 0; r < kBpR; r++) acc[r] = float2v{0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < BT; k++) {
+        float2v pv[kBpR];  // the products first, then the sums: no sum reads the product just made
+#pragma unroll
+        for (int r = 0; r < kBpR; r++) pv[r] = float2v{t.c[k].x, t.c[k].y} * win[r + BT - 1 - k];  // output j0 + 4 tid + r, tap k
+#pragma unroll
+        for (int r = 0; r < kBpR; r++) acc[r] = acc[r] + pv[r];
+        // tap-outer order kept (the accumulators pinned tap by tap, or LLVM sinks each output's
+        // chain whole to its store): the kBpR chains interleave, so no packed result is read by
+        // the next instruction (that costs a wait state on gfx950)
+        asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]));
+    }
+    const long long j = j0 + (long long)kBpR * tid;
+#pragma unroll
+    for (int r = 0; r < kBpR; r++) {
+        if (j + r < L.n_if) {
+            L.channel[(size_t)s * L.n_if + j + r] = acc[r].x;
+            L.carrier[(size_t)s * L.n_if + j + r] = acc[r].y;
+        }
+    }
 }
 
 __global__ void bpf_pair_generic(StereoLaunch L, BpTaps t) {
@@ -57,8 +114,8 @@ __global__ void bpf_pair_generic(StereoLaunch L, BpTaps t) {
     const float* x = L.demod + (size_t)s * L.demod_stride + L.hist + j;
     float a = 0.0f, b = 0.0f;
     for (int k = 0; k < L.bp_taps; k++) {
-        const float pa = t.ch[k] * x[-k];
-        const float pb = t.ca[k] * x[-k];
+        const float pa = t.c[k].x * x[-k];
+        const float pb = t.c[k].y * x[-k];
         a = a + pa;
         b = b + pb;
     }
@@ -619,12 +676,13 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
 }
 
 // One thread per (batch, stream): NB exact steps from the recorded start, compared bit for
-// bit.  `major`: the side data's layout (stream-major for the split kernels, see launch_pll).
+// bit.  The batch's side data (1/v, step x trigOffset) is recomputed, not read back: the kernel
+// then reads only the input, the runner's trigArgs and records (125 vs 210 us a segment at
+// 1,024 streams).
 template <int NB>
 __global__ void __launch_bounds__(64) pll_check_kernel(const float* io, int n, size_t stride, double step,
                                                        float norm_bw, const float* st, const float* out_base,
-                                                       size_t ostride, int* fail, const float2* rec, size_t rb,
-                                                       const double* side, size_t seg, int n_streams, bool major) {
+                                                       size_t ostride, int* fail, const float2* rec, size_t rb) {
     const int s = blockIdx.y;
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     const int nb = n / NB;
@@ -642,26 +700,33 @@ __global__ void __launch_bounds__(64) pll_check_kernel(const float* io, int n, s
     PllState p{S[0], S[1], S[2], S[3], t0};
     PllCtx ctx{};
     ctx.valid = false;
-    if (b > 0) {
-        const PllPair r = pll_state_at_batch(rec[(size_t)s * rb + b - 1], t0, b, NB, o[-1]);
-        p = r.p;
-        ctx = r.ctx;
-    }
     const DeviceLib lib;
+    if (b > 0) {  // inline: no call, no scratch frame for the returned state
+        const float2 rb1 = rec[(size_t)s * rb + b - 1];
+        pll_state_at(p, ctx, rb1.x, rb1.y, t0, (long long)b * NB, o[-1], lib);
+    }
     bool same = true;
     bool done = false;
-    if (ctx.valid) {  // the batch on the certified fast path (~2.5x cheaper than 16 pll_step)
+    // pr_j = step trig_j exactly as pll_side forms it (trig_j = min(t0 + j + 1, 2^24), integer-
+    // valued t0 checked above), recomputed instead of read back: it rises with j, so the batch's
+    // last value decides whether any is out of the fast path's range (pll_side's NaN)
+    const double t0d = (double)t0;
+    const double pr_last = step * fmin(t0d + (double)((long long)b * NB + NB), (double)kPllTrigStick);
+    if (ctx.valid && fabs(pr_last) < kPllMaxPr) {  // the certified fast path (~2.5x cheaper than 16 pll_step)
         float v[NB], c[NB];
         double iv[NB], pr[NB];
-        const double* siv = side;
-        const double* spr = side + seg * (size_t)n_streams;
 #pragma unroll
         for (int j = 0; j < NB; j++) {
             const size_t jj = (size_t)b * NB + j;
-            const size_t a = major ? (size_t)s * seg + jj : (jj / 2 * n_streams + s) * 2 + jj % 2;
             v[j] = x[j];
-            iv[j] = siv[a];
-            pr[j] = spr[a];
+            // 1/v recomputed too (reciprocal + one Newton step, ~2^-46 relative; pll_side's NaN
+            // outside [kPllMinV, 1e300)): the batch's bound takes |Y/v| (|delta| + |eta|) with
+            // |Y/v| <= 2^-23, so eta = 2^-46 adds ~2^-69 to kPllEBatch's 2e-14 (pll_math.h)
+            const double vd = (double)v[j];
+            const double r0 = __builtin_amdgcn_rcp(vd);
+            const double r1 = fma(r0, fma(-vd, r0, 1.0), r0);
+            iv[j] = (fabs(vd) >= (double)kPllMinV && fabs(vd) < 1.0e300) ? r1 : (double)NAN;
+            pr[j] = step * fmin(t0d + (double)(jj + 1), (double)kPllTrigStick);
         }
         const PllState p0 = p;
         const PllCtx c0 = ctx;
@@ -914,12 +979,16 @@ int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s) {
     if (L.n_if <= 0) return 0;
     if (L.bp_taps > kBpMax) return -1;
     BpTaps t{};
-    for (int k = 0; k < L.bp_taps; k++) {
-        t.ch[k] = L.ch_c[k];
-        t.ca[k] = L.ca_c[k];
-    }
+    for (int k = 0; k < L.bp_taps; k++) t.c[k] = make_float2(L.ch_c[k], L.ca_c[k]);
     const dim3 grid((L.n_if + 255) / 256, n_streams), block(256);
-    if (L.bp_taps == 51)
+    static const bool tiled = [] {  // FMRX_BPF_TILE=0: the per-output kernel (A/B measurements)
+        const char* e = std::getenv("FMRX_BPF_TILE");
+        return !(e && e[0] == '0');
+    }();
+    if (L.bp_taps == 51 && L.hist >= 50 && tiled)
+        hipLaunchKernelGGL(bpf_pair_tile_kernel<51>, dim3((L.n_if + kBpTile - 1) / kBpTile, n_streams), dim3(kBpThreads),
+                           0, s, L, t);
+    else if (L.bp_taps == 51)
         hipLaunchKernelGGL(bpf_pair_kernel<51>, grid, block, 0, s, L, t);
     else
         hipLaunchKernelGGL(bpf_pair_generic, grid, block, 0, s, L, t);
@@ -1009,7 +1078,7 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
             const int nb = m / kPllBatch;
             if (nb > 0)
                 hipLaunchKernelGGL(pll_check_kernel<kPllBatch>, dim3((nb + 63) / 64, n_streams), dim3(64), 0, s, x, m,
-                                   stride, step, norm_bw, st, args, seg, fail, rec, rb, side, seg, n_streams, spw <= 4);
+                                   stride, step, norm_bw, st, args, seg, fail, rec, rb);
         }
         if (spw <= 4)
             hipLaunchKernelGGL((pll_kernel<kPllBatch, true>), grid, block, 0, s, x, m, n_streams, spw, stride,
