@@ -144,7 +144,12 @@ __device__ inline void mono_share(const MonoLaunch& L, int w, int n_chunks, int*
 // SIMD, the audio FIR pipelined into the RF tap loop, staggered workgroup starts.
 // AU > 1: the audio stage is the rational resampler of modes 2/3 (up AU, down AD; 51 taps
 // per output phase of a 51*AU-tap prototype read from L.audio_coeff).
-template <int T, int D, int AD, int NT, int R, int PD, int ABL = 0, int TR = 0, int AU = 1>
+// Z0 (bit 1: RF, bit 2: the windowed audio FIR): tap 0 of the context's designed filter is
+// +-0 (filter.cpp:33's window sin(0)^2 = 0 zeroes h[0] of every design), so its products are
+// +-0 and the reference's sum 0.0f + (+-0) leaves +0 -- the state the accumulator starts in: the
+// tap is skipped, bit for bit (inputs are finite: u8 samples, demod quotients).  The host
+// selects it only after checking h[0] == +-0.
+template <int T, int D, int AD, int NT, int R, int PD, int ABL = 0, int TR = 0, int AU = 1, int Z0 = 0>
 __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps taps) {
     using C = MonoCfg<T, D, AD, NT, R>;
     constexpr int CIF = C::CIF, P = C::P, H = C::H, S = C::S, G = C::G, NLD = C::NLD;
@@ -323,7 +328,7 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int k = 2 * j - 1 + h;
-                if (k >= 0) {
+                if (k >= ((Z0 & 1) ? 1 : 0)) {
                     const float2 cj = TR ? creg[TR ? j : 0] : cc[j];
                     const float ck = h == 0 ? cj.x : cj.y;
 #pragma unroll
@@ -477,7 +482,7 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                     const float2* base = dwi + woff0 + AD * tid;
                     float2v a2 = {0.0f, 0.0f};
 #pragma unroll
-                    for (int k = 0; k < ((ABL & 2) != 0 ? 1 : kAudioTaps); k++) {
+                    for (int k = (Z0 & 2) ? 1 : 0; k < ((ABL & 2) != 0 ? 1 : kAudioTaps); k++) {
                         const float2 xs = base[kAH - k];
                         const float2v p = float2v{xs.x, xs.y} * atab[k];
                         a2 = a2 + p;
@@ -521,12 +526,15 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     }
 }
 
-template <int T, int D, int AD, int NT, int R, int PD, int TR = 0, int AU = 1>
+template <int T, int D, int AD, int NT, int R, int PD, int TR = 0, int AU = 1, int Z0 = 0>
 int launch_variant(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStream_t s) {
-    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD, 0, TR, AU>), dim3(n_streams * L.segs), dim3(NT), 0,
+    hipLaunchKernelGGL((mono_fused_kernel<T, D, AD, NT, R, PD, 0, TR, AU, Z0>), dim3(n_streams * L.segs), dim3(NT), 0,
                        s, L, taps);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// h[0] == +-0 (Z0 above)
+bool tap0_zero(float h0) { return (__builtin_bit_cast(uint32_t, h0) & 0x7FFFFFFFu) == 0; }
 
 // Tunables.  The default was picked by measurement on MI355X (tools/tune_list.py); the other
 // variants stay compiled for the tuning sweep (FMRX_MONO_VARIANT=<index>).
@@ -585,6 +593,9 @@ int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_de
         // modes 2/3 with the rational resampler fused (the default kernel shape; mode 3's odd
         // decimation keeps R = 2)
         if (rf_decim == 10 && audio_up == 147 && audio_down == 800) {
+            const bool z = tap0_zero(taps.rf[0]);
+            if (rf_taps == 51 && z) return launch_variant<51, 10, 800, 64, 3, 4, 1, 147, 1>(L, n_streams, taps, s);
+            if (rf_taps == 101 && z) return launch_variant<101, 10, 800, 64, 3, 4, 1, 147, 1>(L, n_streams, taps, s);
             if (rf_taps == 51) return launch_variant<51, 10, 800, 64, 3, 4, 1, 147>(L, n_streams, taps, s);
             if (rf_taps == 101) return launch_variant<101, 10, 800, 64, 3, 4, 1, 147>(L, n_streams, taps, s);
         }
@@ -617,9 +628,16 @@ int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_de
             default: break;
         }
     }
-#define FMRX_V(T_, D_, AD_, I_, NT_, R_, PD_, TR_)                                         \
-    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == I_)                  \
-        return launch_variant<T_, D_, AD_, NT_, R_, PD_, TR_>(L, n_streams, taps, s);
+    // the default variant skips tap 0 (Z0) when the designs have h[0] = +-0 (always, for the
+    // context's own taps; both FIRs then), the sweep variants keep it
+    const bool z0 = tap0_zero(taps.rf[0]) && (!L.audio || tap0_zero(taps.audio[0]));
+#define FMRX_V(T_, D_, AD_, I_, NT_, R_, PD_, TR_)                                              \
+    if (rf_taps == T_ && rf_decim == D_ && audio_down == AD_ && vi == I_) {                     \
+        if (I_ == kDefaultVariant && z0)                                                        \
+            return launch_variant<T_, D_, AD_, NT_, R_, PD_, TR_, 1, (I_ == kDefaultVariant ? 3 : 0)>(L, n_streams, \
+                                                                                                      taps, s);  \
+        return launch_variant<T_, D_, AD_, NT_, R_, PD_, TR_>(L, n_streams, taps, s);           \
+    }
 #define FMRX_ALL(T_, D_, AD_)              \
     FMRX_V(T_, D_, AD_, 0, 256, 3, 3, 0)   \
     FMRX_V(T_, D_, AD_, 1, 128, 3, 3, 0)   \
