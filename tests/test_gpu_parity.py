@@ -506,9 +506,10 @@ def test_pll_primitive_states(fmrx, orc, trig, phase, freq, fs, n, offset):
         assert same(st.cpu().numpy(), want_st)
 
 
+@pytest.mark.parametrize("freq,nco_scale", [(19000, 2.0), (114000, 0.5)])  # pilot (project.cpp:166), RDS (:226)
 @pytest.mark.parametrize("inject", [None, "3"])
 @pytest.mark.parametrize("sat", ["1", "0"])
-def test_pll_saturated_runner(fmrx, orc, monkeypatch, inject, sat):
+def test_pll_saturated_runner(fmrx, orc, monkeypatch, inject, sat, freq, nco_scale):
     """A segment that starts with trigOffset stuck at 2^24 (filter.cpp:165-166 in float, 69.9 s
     into a stream): the speculative runner skips the sin/cos of repeated trigArgs; with and
     without that skipping, and with a corrupted runner batch (check + certified resume)."""
@@ -518,14 +519,14 @@ def test_pll_saturated_runner(fmrx, orc, monkeypatch, inject, sat):
     n = 20000
     rng = np.random.default_rng(24)
     t = np.arange(n)
-    x = (0.1 * np.cos(2 * np.pi * 19000 / 240000 * t + 0.3) + 0.01 * rng.standard_normal(n)).astype(np.float32)
+    x = (0.1 * np.cos(2 * np.pi * freq / 240000 * t + 0.3) + 0.01 * rng.standard_normal(n)).astype(np.float32)
     st0 = np.array([2e-4, 1.7, 0.6, 0.8, 1.0, 16777216.0], np.float32)
-    want_x, want_st = orc.pll(x, 19000, 240000, 2.0, 0.0, 0.01, st0)
+    want_x, want_st = orc.pll(x, freq, 240000, nco_scale, 0.0, 0.01, st0)
     with fmrx.Receiver(0, fmrx.STEREO) as rx:
         buf = _d(x)
         st = _d(st0)
         torch.cuda.synchronize()
-        rx.pll(buf.data_ptr(), n, 19000, 240000, 2.0, 0.0, 0.01, st.data_ptr())
+        rx.pll(buf.data_ptr(), n, freq, 240000, nco_scale, 0.0, 0.01, st.data_ptr())
         rx.synchronize()
         assert same(buf.cpu().numpy(), want_x)
         assert same(st.cpu().numpy(), want_st)
