@@ -203,6 +203,13 @@ int fmrx_test_pll_fallback(fmrx_ctx* ctx, int kind, const float* d_a, const floa
  * can launch (n_streams x 256 x resident workgroups per CU).  d_stamps = NULL turns it off. */
 int fmrx_debug_mono_stamps(fmrx_ctx* ctx, unsigned long long* d_stamps, size_t n_workgroups, size_t* needed);
 
+/* ---- diagnostic: speculative PLL counters ------------------------------------------------ */
+/* With d_counts set (2 u64 on the device, zeroed and owned by the caller), every speculative  *
+ * PLL segment of the stereo path and of fmrx_pll adds the runner's 16-step batches that did    *
+ * not verify (resumed on the certified path) to d_counts[0] and the batches checked to         *
+ * d_counts[1].  Results are unchanged.  d_counts = NULL turns it off.                          */
+int fmrx_debug_pll_stats(fmrx_ctx* ctx, unsigned long long* d_counts);
+
 #ifdef __cplusplus
 }
 #endif

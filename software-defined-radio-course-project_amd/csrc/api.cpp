@@ -118,6 +118,7 @@ struct fmrx_ctx {
     size_t ev_used = 0;
     bool timing = false;
     unsigned long long* stamps = nullptr;  // fmrx_debug_mono_stamps (diagnostic)
+    unsigned long long* pll_stats = nullptr;  // fmrx_debug_pll_stats (diagnostic)
 };
 
 namespace {
@@ -373,7 +374,7 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
     // project.cpp:166: PLL(carrier, 19000, if_fs, 2, 0, 0.01, ...)
     if ((rc = c->d_pll_side.ensure(pll_side_doubles((int)n_if, ns)))) return rc;
     if (launch_pll(c->d_carrier.p, (int)n_if, ns, n_if, 19000.0f, (float)c->geo.if_fs, 2.0f, 0.0f,
-                   0.01f, c->d_pll.p, c->d_pll_side.p, c->stream))
+                   0.01f, c->d_pll.p, c->d_pll_side.p, c->stream, c->pll_stats))
         return fail(FMRX_EHIP, "PLL launch failed");
     AudioLaunch A{};
     A.demod = c->d_demod.p;
@@ -959,7 +960,7 @@ int fmrx_pll(fmrx_ctx* c, float* d_io, int n, float freq, float fs, float nco_sc
     HIPCHK(hipMemcpyAsync(c->d_scratch.p, d_st, 6 * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
     if ((rc = c->d_pll_side.ensure(pll_side_doubles(n, 1)))) return rc;
     if (launch_pll(d_io, n, 1, (size_t)n, freq, fs, nco_scale, phase_adjust, norm_bw, c->d_scratch.p,
-                   c->d_pll_side.p, c->stream))
+                   c->d_pll_side.p, c->stream, c->pll_stats))
         return fail(FMRX_EHIP, "launch failed");
     HIPCHK(hipMemcpyAsync(d_st, c->d_scratch.p, 6 * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
     return FMRX_OK;
@@ -1040,5 +1041,13 @@ int fmrx_debug_mono_stamps(fmrx_ctx* c, unsigned long long* d_stamps, size_t n_w
     if (d_stamps && needed && n_workgroups < *needed)
         return fail(FMRX_EINVAL, "stamp buffer holds %zu workgroups, up to %zu launch", n_workgroups, *needed);
     c->stamps = d_stamps;
+    return FMRX_OK;
+}
+
+// Diagnostic: speculative-PLL counters of the stereo and PLL calls (launch_pll's spec_stats).
+int fmrx_debug_pll_stats(fmrx_ctx* c, unsigned long long* d_counts) {
+    CtxLock lock_(c);
+    if (!c) return fail(FMRX_EINVAL, "null context");
+    c->pll_stats = d_counts;
     return FMRX_OK;
 }

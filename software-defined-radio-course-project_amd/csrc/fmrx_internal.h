@@ -88,10 +88,13 @@ struct StereoLaunch {
 int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s);
 // PLL over n samples of n_streams streams (state st, 8 floats per stream), then the NCO
 // (filter.cpp:136-174).  side: device scratch of pll_side_doubles(n, n_streams) doubles.
+// spec_stats (diagnostic, may be null): the speculative path adds the runner batches that did
+// not verify to spec_stats[0] and the batches checked to spec_stats[1].
 constexpr size_t kPllSeg = (size_t)1 << 18;  // at most this many samples per stream per PLL segment
 size_t pll_side_doubles(int n, int n_streams);
 int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
-               float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s);
+               float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s,
+               unsigned long long* spec_stats = nullptr);
 
 // test hook: the PLL's fallback libm on device (kind 0 sincos, 1 atan2, 2 NCO cos)
 int launch_pll_fallback_test(int kind, const float* a, const float* b, size_t n, float* out, hipStream_t s);

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 #include "dsp_device.h"
 #include "fmrx_internal.h"
@@ -275,7 +276,7 @@ template <int NB, bool SPLIT>
 __global__ void __launch_bounds__(256) pll_kernel(float* io, int n, int n_streams, int spw, size_t stride,
                                                  const double* side, size_t seg, double step, float norm_bw,
                                                  float* st, float* out_base, size_t ostride, const int* fail,
-                                                 const float2* rec, size_t rb) {
+                                                 const float2* rec, size_t rb, unsigned long long* stats) {
     const int t = threadIdx.x & 63;
     const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int s_lane = wave * spw + (SPLIT ? ((t >> 4) & (spw - 1)) : (t & (spw - 1)));
@@ -300,6 +301,11 @@ __global__ void __launch_bounds__(256) pll_kernel(float* io, int n, int n_stream
     int b0 = 0;
     if (fail) {  // after the speculative runner: x is aligned (the host checked)
         int m = fail[s];
+        if (stats && owner) {  // diagnostic counters (fmrx_debug_pll_stats), one atomic per stream
+            const int nbs = n / NB;
+            atomicAdd(stats, (unsigned long long)(nbs - m));
+            atomicAdd(stats + 1, (unsigned long long)nbs);
+        }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o));
         b0 = m;
@@ -485,6 +491,13 @@ __device__ inline double row_bcast(double v) {
     return __builtin_bit_cast(double, (long long)__builtin_amdgcn_mov_dpp(bits, 0x150 + L, 0xF, 0xF, false));
 }
 
+// f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>): a loop whose index is a
+// compile-time constant in the body (row_bcast's lane)
+template <class F, int... J>
+__device__ inline void unroll_ic(F&& f, std::integer_sequence<int, J...>) {
+    (f(std::integral_constant<int, J>{}), ...);
+}
+
 template <int NB>
 __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int n, int n_streams, int spw,
                                                            size_t stride, const double* side, size_t seg, double step,
@@ -519,6 +532,124 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
     if (nb < 2) return;
     // SAT (trigOffset stuck at 2^24 for the whole segment, one stream a wave; see run below)
     const bool sat = sat_ok && spw == 1 && p.trig == kPllTrigStick;
+    const double prd = step * (double)kPllTrigStick;  // pll_side's step x trigOffset, stuck
+    if (sat && sat_ok == 1 && fabs(prd) < kPllMaxPr) {
+        // Saturated segment, step-parallel form.  While trigArg repeats, the feedback (fc, nfs,
+        // sn, cs) and the two offsets -B(x, 0), -B(x, 1/2) stay fixed, so a step's error
+        // e_j = float(Y(v_j) / v_j - B(x, h_j)) does not depend on the loop state: lane l of the
+        // row computes (Ki e, Kp e) of step l of the batch for all 16 steps at once, and the serial
+        // chain per step is one row broadcast of that pair, the three float updates, trigArg
+        // (pr is the constant step 2^24) and the repeat test.  When trigArg moves, the sin/cos
+        // and offsets are refreshed (lanes 0/1 sin/cos, lanes 2/3 the offsets) and the pairs of
+        // the batch's remaining steps recomputed.  Half turn h_j = 1/2 [iv_j < 0]: iv's sign bit.
+        const int l = t & 15;
+        const bool off = l == 2 || l == 3;
+        const double C1 = off ? kInv2Pi : kInvPio2;
+        const double Chi = off ? k2PiHi : kPio2Hi;
+        const double Clo = off ? k2PiLo : kPio2Lo;
+        const double Hc = l == 2 ? 0.5 : 0.0;  // lane 2 -B(x, 1/2), lane 3 -B(x, 0)
+        const double* ivs = side + (size_t)s * seg;
+        const int q0 = ctx.q;
+        const float u0 = (q0 & 1) ? p.fbQ : p.fbI, w0 = (q0 & 1) ? p.fbI : -p.fbQ;
+        float fc = (q0 & 2) ? -u0 : u0, nfs = (q0 & 2) ? -w0 : w0;
+        double sn = ctx.sn, cs = ctx.cs;
+        double nB0 = -pll_offset_h(ctx.x, 0.0), nB1 = -pll_offset_h(ctx.x, 0.5);
+        float integ = p.integ, phase = p.phase;
+        uint32_t prev = __builtin_bit_cast(uint32_t, (float)ctx.x);
+        // (Ki e, Kp e) of this lane's step from the current feedback
+        auto ke_of = [&](float vl, double ivl) -> double {
+            const float2v ab = float2v{fc, nfs} * vl;
+            const double Y = fma((double)ab.x, sn, (double)ab.y * cs);
+            const uint64_t ib = __builtin_bit_cast(uint64_t, ivl);
+            const uint64_t m = (uint64_t)(uint32_t)((int)(uint32_t)(ib >> 32) >> 31) * 0x100000001ull;
+            const double nB = __builtin_bit_cast(double, (m & __builtin_bit_cast(uint64_t, nB1)) |
+                                                             (~m & __builtin_bit_cast(uint64_t, nB0)));
+            const float e = (float)fma(Y, ivl, -nB);
+            return __builtin_bit_cast(double, float2v{Ki, Kp} * e);
+        };
+        // fresh feedback and offsets from trigArg a (lanes 0/1 sin/cos, lanes 2/3 the offsets)
+        auto refresh = [&](uint32_t a_bits) {
+            const double xa = (double)__builtin_bit_cast(float, a_bits);
+            const double tq = rint(fma(xa, C1, Hc)) - Hc;
+            const double w = fma(-tq, Clo, fma(-tq, Chi, xa));
+            nB1 = row_bcast<2>(w);
+            nB0 = row_bcast<3>(w);
+            const double W = split_w_horner(w * w, sc);
+            sn = row_bcast<0>(w * W);
+            cs = row_bcast<1>(W);
+            fc = (float)cs;
+            nfs = -(float)sn;
+        };
+        // The repeat test of step j is branched on at step j + 1 (a branch on a compare just
+        // made waits ~40 cycles for it): step j + 1 is computed with the old pairs first and,
+        // when trigArg moved at step j, redone after the refresh.
+        uint64_t moved = 0;
+        // one batch; vb, ivb: this lane's step data (step l of the batch)
+        auto batch = [&](int b, float vb, double ivb) __attribute__((always_inline)) {
+            double ke = ke_of(vb, ivb);
+            float o[NB];
+            unroll_ic(
+                [&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    const float integ0 = integ, phase0 = phase;
+                    const uint32_t prev0 = prev;
+                    uint64_t moved_j;
+                    auto step_j = [&]() {
+                        // the pair as two 32-bit halves (as a float2 the SLP vectorizer pairs
+                        // the adds into packed ops, each read back after a wait state)
+                        const uint64_t kb = __builtin_bit_cast(uint64_t, row_bcast<j>(ke));
+                        integ = integ0 + __builtin_bit_cast(float, (uint32_t)kb);
+                        phase = phase0 + (__builtin_bit_cast(float, (uint32_t)(kb >> 32)) + integ);
+                        const float arg = (float)(prd + (double)phase);
+                        o[j] = arg;
+                        prev = __builtin_bit_cast(uint32_t, arg);
+                        moved_j = __builtin_amdgcn_ballot_w64(prev != prev0);
+                    };
+                    step_j();
+                    if (__builtin_expect(moved != 0, 0)) {  // trigArg moved at step j - 1
+                        refresh(prev0);
+                        ke = ke_of(vb, ivb);
+                        step_j();
+                    }
+                    moved = moved_j;
+                },
+                std::make_integer_sequence<int, NB>{});
+            phase += (inject >= 0 && b == 1 + (inject + s) % (nb - 1)) ? 1.0e-3f : 0.0f;  // test hook
+            float* ob = out + b * NB;
+#pragma unroll
+            for (int q = 0; q < NB / 4; q++)
+                reinterpret_cast<float4*>(ob)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
+            rec[(size_t)s * rb + b] = make_float2(integ, phase);
+        };
+        // The lane's step data is loaded about three batches ahead (a batch here is ~800
+        // cycles, shorter than a load from HBM): ring slot u serves batches 1 + u (mod 4) and is
+        // refilled at the end of its batch, after its last read, so the load lands in place.
+        float vq[4];
+        double ivq[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int bq = 1 + u < nb ? 1 + u : nb - 1;
+            vq[u] = x[bq * NB + l];
+            ivq[u] = ivs[bq * NB + l];
+        }
+        // landed before the loop: the loop top then waits only for the slot it reads (a load
+        // issued last here would make the waitcnt pass wait for every load at each iteration)
+        __builtin_amdgcn_s_waitcnt(0);
+        int b0 = 1;
+        for (; b0 + 3 < nb; b0 += 4) {
+            unroll_ic(
+                [&](auto uc) {
+                    constexpr int u = decltype(uc)::value;
+                    batch(b0 + u, vq[u], ivq[u]);
+                    const int bq = b0 + u + 4 < nb ? b0 + u + 4 : nb - 1;
+                    vq[u] = x[bq * NB + l];
+                    ivq[u] = ivs[bq * NB + l];
+                },
+                std::make_integer_sequence<int, 4>{});
+        }
+        for (; b0 < nb; b0++) batch(b0, x[b0 * NB + l], ivs[b0 * NB + l]);
+        return;
+    }
     // reduction constants: 2 pi on the offset lanes (lane 2; with SAT lane 3 too), pi/2 on the
     // sin/cos lanes
     const bool two_pi = b_lane || (sat && (t & 15) == 3);
@@ -1018,7 +1149,8 @@ size_t pll_side_doubles(int n, int n_streams) {
 // the first batch that did not verify) unless FMRX_PLL_SPEC=0 or the streams' rows are not
 // 16-byte aligned; the plain path is pll_kernel in place.
 int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
-               float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s) {
+               float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s,
+               unsigned long long* spec_stats) {
     if (n <= 0) return 0;
     const size_t seg = pll_seg_len(n, n_streams);
     const size_t rb = seg / kPllBatch;
@@ -1042,10 +1174,11 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         return e ? std::atoi(e) : -1;
     }();
     const bool spec = spec_env && (reinterpret_cast<uintptr_t>(io) & 15) == 0 && stride % 4 == 0;
-    // FMRX_PLL_SAT=0 (measurements, tests): no sin/cos skipping once trigOffset has stuck at 2^24
+    // FMRX_PLL_SAT=0 (measurements, tests): no sin/cos skipping once trigOffset has stuck at 2^24;
+    // =2: the per-step form (cached offsets) instead of the step-parallel one
     const int sat_ok = [] {
         const char* e = std::getenv("FMRX_PLL_SAT");
-        return (e && e[0] == '0') ? 0 : 1;
+        return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
     }();
     int spw = 1;
     while (spw < 64 && (long long)spw * n_simd < n_streams) spw *= 2;
@@ -1082,10 +1215,12 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         }
         if (spw <= 4)
             hipLaunchKernelGGL((pll_kernel<kPllBatch, true>), grid, block, 0, s, x, m, n_streams, spw, stride,
-                               side, seg, step, norm_bw, st, out, ostride, spec ? fail : nullptr, rec, rb);
+                               side, seg, step, norm_bw, st, out, ostride, spec ? fail : nullptr, rec, rb,
+                               spec_stats);
         else
             hipLaunchKernelGGL((pll_kernel<kPllBatch, false>), grid, block, 0, s, x, m, n_streams, spw, stride,
-                               side, seg, step, norm_bw, st, out, ostride, spec ? fail : nullptr, rec, rb);
+                               side, seg, step, norm_bw, st, out, ostride, spec ? fail : nullptr, rec, rb,
+                               spec_stats);
         hipLaunchKernelGGL(pll_nco_kernel, dim3((m + 255) / 256, n_streams), dim3(256), 0, s, x, m, stride, out,
                            ostride, nco_scale, phase_adjust, st);
     }

@@ -84,6 +84,7 @@ PROTOTYPES = {
     "fmrx_synth_device": (C.c_int, [_vp, C.c_uint64, C.c_int, C.c_uint64, _sz, _vp]),
     "fmrx_test_pll_fallback": (C.c_int, [_vp, C.c_int, _vp, _vp, _sz, _vp]),
     "fmrx_debug_mono_stamps": (C.c_int, [_vp, _vp, _sz, C.POINTER(_sz)]),
+    "fmrx_debug_pll_stats": (C.c_int, [_vp, _vp]),
 }
 
 _lib = None
@@ -350,6 +351,11 @@ class Receiver:
         need = _sz()
         _check(lib().fmrx_debug_mono_stamps(self.h, d_stamps, n_workgroups, C.byref(need)))
         return need.value
+
+    def debug_pll_stats(self, d_counts: int | None) -> None:
+        """Diagnostic speculative-PLL counters (fmrx.h): d_counts[0] += runner batches that did
+        not verify, d_counts[1] += batches checked (2 u64 on the device); None turns it off."""
+        _check(lib().fmrx_debug_pll_stats(self.h, d_counts))
 
 
 def build() -> None:

@@ -409,9 +409,17 @@ def test_pll_speculation_fallbacks(fmrx, orc, monkeypatch, env, n_streams, nb):
     recipes = [("synth:%d" if s % 3 else "rand:%d") % (900 + s) for s in range(n_streams)]
     ins = np.stack([iqgen.make(r, nb * bb) for r in recipes])
     with fmrx.Receiver(0, fmrx.STEREO, n_streams=n_streams) as rx:
+        counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+        rx.debug_pll_stats(counts.data_ptr())
         out = np.atleast_2d(rx.process(ins))
+        rx.debug_pll_stats(None)
         if n_streams == 1:
             out2 = np.atleast_2d(rx.process(ins))  # a second call from the carried state
+    resumed, checked = counts.cpu().tolist()
+    if "FMRX_PLL_SPEC_INJECT" in env:  # every stream's corrupted batch was caught and resumed
+        assert checked > 0 and resumed >= n_streams, (resumed, checked)
+    else:  # the plain launch: nothing speculative ran
+        assert (resumed, checked) == (0, 0)
     for s in sorted({0, min(1, n_streams - 1), n_streams // 2, n_streams - 1}):
         assert np.array_equal(out[s], orc.run(0, 51, ins[s], ["pcm"])["pcm"]), s
     if n_streams == 1:
@@ -508,11 +516,13 @@ def test_pll_primitive_states(fmrx, orc, trig, phase, freq, fs, n, offset):
 
 @pytest.mark.parametrize("freq,nco_scale", [(19000, 2.0), (114000, 0.5)])  # pilot (project.cpp:166), RDS (:226)
 @pytest.mark.parametrize("inject", [None, "3"])
-@pytest.mark.parametrize("sat", ["1", "0"])
+@pytest.mark.parametrize("sat", ["1", "2", "0"])
 def test_pll_saturated_runner(fmrx, orc, monkeypatch, inject, sat, freq, nco_scale):
     """A segment that starts with trigOffset stuck at 2^24 (filter.cpp:165-166 in float, 69.9 s
-    into a stream): the speculative runner skips the sin/cos of repeated trigArgs; with and
-    without that skipping, and with a corrupted runner batch (check + certified resume)."""
+    into a stream): the speculative runner's saturated forms (1 step-parallel, 2 per-step with
+    cached offsets, 0 none), and a corrupted runner batch (check + certified resume).  The
+    speculation counters must show every batch verified without the corruption -- a runner
+    that disagrees with the exact path would otherwise pass here, fixed up by the resume."""
     monkeypatch.setenv("FMRX_PLL_SAT", sat)
     if inject is not None:
         monkeypatch.setenv("FMRX_PLL_SPEC_INJECT", inject)
@@ -525,11 +535,17 @@ def test_pll_saturated_runner(fmrx, orc, monkeypatch, inject, sat, freq, nco_sca
     with fmrx.Receiver(0, fmrx.STEREO) as rx:
         buf = _d(x)
         st = _d(st0)
+        counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+        rx.debug_pll_stats(counts.data_ptr())
         torch.cuda.synchronize()
         rx.pll(buf.data_ptr(), n, freq, 240000, nco_scale, 0.0, 0.01, st.data_ptr())
         rx.synchronize()
+        rx.debug_pll_stats(None)
         assert same(buf.cpu().numpy(), want_x)
         assert same(st.cpu().numpy(), want_st)
+        resumed, checked = counts.cpu().tolist()
+        assert checked == n // 16
+        assert (resumed > 0) if inject is not None else (resumed == 0), (resumed, checked)
 
 
 def test_quantize_and_elementwise(fmrx, orc):
