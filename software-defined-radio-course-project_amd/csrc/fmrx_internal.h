@@ -96,6 +96,12 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
                float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s,
                unsigned long long* spec_stats = nullptr);
 
+// pll_sat.hip: the saturated-segment runner over a launch_pll segment (pll_spec_lane_kernel's grid
+// and arguments; it runs the streams that one leaves to it)
+void launch_pll_sat(dim3 grid, dim3 block, hipStream_t s, const float* io, int n, int n_streams, int spw,
+                    size_t stride, const double* side, size_t seg, double step, float norm_bw, const float* st,
+                    float* out, size_t ostride, int* fail, float2* rec, size_t rb, int inject);
+
 // test hook: the PLL's fallback libm on device (kind 0 sincos, 1 atan2, 2 NCO cos)
 int launch_pll_fallback_test(int kind, const float* a, const float* b, size_t n, float* out, hipStream_t s);
 

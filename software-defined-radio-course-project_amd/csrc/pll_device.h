@@ -1,0 +1,97 @@
+// pll_device.h — device pieces of the stereo pilot PLL (src/filter.cpp:136-174) shared by
+// stereo.hip (the runners, check and resume kernels) and pll_sat.hip (the saturated-segment
+// runner, built as its own translation unit: see the Makefile).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <utility>
+
+#include "pll_cr.h"
+#include "pll_math.h"
+
+namespace fmrx {
+namespace {
+
+// src/filter.cpp:136-174 PLL.  A nonlinear recurrence: strictly serial in time, so one lane
+// per stream.  Float state; the reference's double atan2 / cos / sin results rounded to
+// float come from pll_math.h's certified fast path (fallback: the full library call).
+// st = {integrator, phaseEst, feedbackI, feedbackQ, ncoOut_state, trigOffset} (stride 8).
+//
+// The recurrence only needs atan2 and sincos; the NCO output cos(trigArg * ncoScale +
+// phaseAdjust) (filter.cpp:170) depends on nothing later, so the serial loop stores trigArg
+// in place and pll_nco_kernel evaluates the NCO for all samples in parallel afterwards.
+// Fallbacks where a certified fast path refuses (~1e-6 of steps), out of line: pll_cr.h's
+// double-double evaluation rounded like glibc (float of the correctly rounded double), pinned to
+// glibc on every refusable sincos argument of the PLL's domain (tools/check_pll_cr.cpp,
+// tests/golden/pll_fallback.npz).  HIP's double sin/cos only beyond |x| >= 2^31, a trigArg no
+// PLL state reaches (|trigArg| < 1e9 wherever the step's product is finite).
+__device__ __noinline__ float atan2_lib(float y, float x) {
+    float e;
+    if (fast_atan2_f(y, x, &e)) return e;
+    return cr::atan2_f(y, x);
+}
+__device__ __noinline__ float2 sincos_lib(float a) {
+    if (!cr::sincos_domain(a))
+        return make_float2(static_cast<float>(sin(static_cast<double>(a))),
+                           static_cast<float>(cos(static_cast<double>(a))));
+    float sv, cv;
+    cr::sincos_f(a, &sv, &cv);
+    return make_float2(sv, cv);
+}
+
+struct DeviceLib {
+    __device__ float atan2f_(float y, float x) const { return atan2_lib(y, x); }
+    __device__ void sincosf_(float a, float* s, float* c) const {
+        const float2 r = sincos_lib(a);
+        *s = r.x;
+        *c = r.y;
+    }
+};
+
+// n exact steps (pll_step with the library fallbacks), out of line: the kernel then holds no
+// calls, so the batch loop's registers are not saved and restored around them.
+struct PllPair {
+    PllState p;
+    PllCtx ctx;
+};
+// `wr` false: compute only.  Lanes of the grid's padding waves (s_lane >= n_streams) recompute
+// the last stream but do not run in lockstep with its own wave, which in the plain launch
+// overwrites the input in place: they must not write what they derived from it.
+__device__ __noinline__ PllPair pll_redo(PllState p, PllCtx ctx, const float* xb, float* ob, int n, float Ki,
+                                         float Kp, double step, bool wr) {
+    const DeviceLib lib;
+#pragma unroll 1
+    for (int j = 0; j < n; j++) {
+        const float a = pll_step(p, ctx, xb[j], Ki, Kp, step, lib);
+        if (wr) ob[j] = a;
+    }
+    return PllPair{p, ctx};
+}
+
+// NB samples per optimistic batch.  Measured (10 s mode-0 stereo): NB = 16 beats 8 and 12.  The
+// certification is ~23 % of the step: without it the loop runs 0.31 s instead of 0.40 s.
+constexpr int kPllBatch = 16;
+
+template <int L>
+__device__ inline double row_bcast(double v) {
+    const long long bits = __builtin_bit_cast(long long, v);
+    return __builtin_bit_cast(double, (long long)__builtin_amdgcn_mov_dpp(bits, 0x150 + L, 0xF, 0xF, false));
+}
+
+// f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>): a loop whose index is a
+// compile-time constant in the body (row_bcast's lane)
+template <class F, int... J>
+__device__ inline void unroll_ic(F&& f, std::integer_sequence<int, J...>) {
+    (f(std::integral_constant<int, J>{}), ...);
+}
+
+// A segment for pll_sat_kernel: one stream a wave and trigOffset stuck at 2^24 from its start
+// (filter.cpp:165-166: trigOffset + 1.0f == trigOffset from there, 69.9 s into a stream at
+// 240 kS/s), so every step's pr is the constant step 2^24 (pll_side).  pll_spec_lane_kernel
+// leaves exactly these streams to it.
+__device__ inline bool pll_sat_segment(int spw, float trig0, double step) {
+    return spw == 1 && trig0 == kPllTrigStick && fabs(step * (double)kPllTrigStick) < kPllMaxPr;
+}
+
+}  // namespace
+}  // namespace fmrx

@@ -18,6 +18,7 @@
 #include "dsp_device.h"
 #include "fmrx_internal.h"
 #include "pll_cr.h"
+#include "pll_device.h"
 #include "pll_math.h"
 
 namespace fmrx {
@@ -124,42 +125,6 @@ __global__ void bpf_pair_generic(StereoLaunch L, BpTaps t) {
     L.carrier[(size_t)s * L.n_if + j] = b;
 }
 
-// src/filter.cpp:136-174 PLL.  A nonlinear recurrence: strictly serial in time, so one lane
-// per stream.  Float state; the reference's double atan2 / cos / sin results rounded to
-// float come from pll_math.h's certified fast path (fallback: the full library call).
-// st = {integrator, phaseEst, feedbackI, feedbackQ, ncoOut_state, trigOffset} (stride 8).
-//
-// The recurrence only needs atan2 and sincos; the NCO output cos(trigArg * ncoScale +
-// phaseAdjust) (filter.cpp:170) depends on nothing later, so the serial loop stores trigArg
-// in place and pll_nco_kernel evaluates the NCO for all samples in parallel afterwards.
-// Fallbacks where a certified fast path refuses (~1e-6 of steps), out of line: pll_cr.h's
-// double-double evaluation rounded like glibc (float of the correctly rounded double), pinned to
-// glibc on every refusable sincos argument of the PLL's domain (tools/check_pll_cr.cpp,
-// tests/golden/pll_fallback.npz).  HIP's double sin/cos only beyond |x| >= 2^31, a trigArg no
-// PLL state reaches (|trigArg| < 1e9 wherever the step's product is finite).
-__device__ __noinline__ float atan2_lib(float y, float x) {
-    float e;
-    if (fast_atan2_f(y, x, &e)) return e;
-    return cr::atan2_f(y, x);
-}
-__device__ __noinline__ float2 sincos_lib(float a) {
-    if (!cr::sincos_domain(a))
-        return make_float2(static_cast<float>(sin(static_cast<double>(a))),
-                           static_cast<float>(cos(static_cast<double>(a))));
-    float sv, cv;
-    cr::sincos_f(a, &sv, &cv);
-    return make_float2(sv, cv);
-}
-
-struct DeviceLib {
-    __device__ float atan2f_(float y, float x) const { return atan2_lib(y, x); }
-    __device__ void sincosf_(float a, float* s, float* c) const {
-        const float2 r = sincos_lib(a);
-        *s = r.x;
-        *c = r.y;
-    }
-};
-
 // Side data of one PLL segment (pll_math.h pll_side): iv, pr for every sample, in
 // parallel, from the trigOffset the segment starts with.  Two arrays of seg x n_streams
 // doubles, sample pairs stream-minor: element (j, s) at (j/2 * n_streams + s) * 2 + j%2, so
@@ -225,26 +190,6 @@ __global__ void __launch_bounds__(256) pll_prep_major_kernel(const float* io, in
     sh[1] = make_double2(0.0, 0.0);
 }
 
-// n exact steps (pll_step with the library fallbacks), out of line: the kernel then holds no
-// calls, so the batch loop's registers are not saved and restored around them.
-struct PllPair {
-    PllState p;
-    PllCtx ctx;
-};
-// `wr` false: compute only.  Lanes of the grid's padding waves (s_lane >= n_streams) recompute
-// the last stream but do not run in lockstep with its own wave, which in the plain launch
-// overwrites the input in place: they must not write what they derived from it.
-__device__ __noinline__ PllPair pll_redo(PllState p, PllCtx ctx, const float* xb, float* ob, int n, float Ki,
-                                         float Kp, double step, bool wr) {
-    const DeviceLib lib;
-#pragma unroll 1
-    for (int j = 0; j < n; j++) {
-        const float a = pll_step(p, ctx, xb[j], Ki, Kp, step, lib);
-        if (wr) ob[j] = a;
-    }
-    return PllPair{p, ctx};
-}
-
 // pll_math.h pll_state_at for the start of batch b (b NB steps into the segment), out of line.
 __device__ __noinline__ PllPair pll_state_at_batch(float2 rec, float t0, int b, int nbatch, float a) {
     PllPair r;
@@ -252,10 +197,6 @@ __device__ __noinline__ PllPair pll_state_at_batch(float2 rec, float t0, int b, 
     return r;
 }
 
-// NB samples per optimistic batch.  Measured (10 s mode-0 stereo): NB = 16 beats 8 and 12.  The
-// certification is ~23 % of the step: without it the loop runs 0.31 s instead of 0.40 s.
-constexpr int kPllBatch = 16;
-//
 // Streams per wave (spw, a power of two <= 64): lane t works on stream blockIdx.x spw + t % spw,
 // and only lanes t < spw store.  The other lanes recompute their stream in lockstep (identical
 // values): a wave with every lane active runs the serial chain ~15 % faster than one with a
@@ -485,19 +426,6 @@ __global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, i
 // the serial chain is a packed op but the first product (a packed f32 result read by the next
 // instruction costs a wait state on gfx950).  ~36 VALU a step, 82 % of the wave's cycles issuing VALU
 // (profiles/r02/runner/).  The result is checked by pll_check_kernel like pll_spec_kernel's.
-template <int L>
-__device__ inline double row_bcast(double v) {
-    const long long bits = __builtin_bit_cast(long long, v);
-    return __builtin_bit_cast(double, (long long)__builtin_amdgcn_mov_dpp(bits, 0x150 + L, 0xF, 0xF, false));
-}
-
-// f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>): a loop whose index is a
-// compile-time constant in the body (row_bcast's lane)
-template <class F, int... J>
-__device__ inline void unroll_ic(F&& f, std::integer_sequence<int, J...>) {
-    (f(std::integral_constant<int, J>{}), ...);
-}
-
 template <int NB>
 __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int n, int n_streams, int spw,
                                                            size_t stride, const double* side, size_t seg, double step,
@@ -519,6 +447,7 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
     const float Kp = norm_bw * static_cast<float>(2.666);
     const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
     PllState p{S[0], S[1], S[2], S[3], S[5]};
+    if (sat_ok && pll_sat_segment(spw, p.trig, step)) return;  // pll_sat_kernel's (pll_sat.hip)
     const int nb = n / NB;
     if (owner) fail[s] = nb;
     PllCtx ctx{};
@@ -530,136 +459,13 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
         if (owner) rec[(size_t)s * rb] = make_float2(p.integ, p.phase);
     }
     if (nb < 2) return;
-    // SAT (trigOffset stuck at 2^24 for the whole segment, one stream a wave; see run below)
-    const bool sat = sat_ok && spw == 1 && p.trig == kPllTrigStick;
-    const double prd = step * (double)kPllTrigStick;  // pll_side's step x trigOffset, stuck
-    if (sat && sat_ok == 1 && fabs(prd) < kPllMaxPr) {
-        // Saturated segment, step-parallel form.  While trigArg repeats, the feedback (fc, nfs,
-        // sn, cs) and the two offsets -B(x, 0), -B(x, 1/2) stay fixed, so a step's error
-        // e_j = float(Y(v_j) / v_j - B(x, h_j)) does not depend on the loop state: lane l of the
-        // row computes (Ki e, Kp e) of step l of the batch for all 16 steps at once, and the serial
-        // chain per step is one row broadcast of that pair, the three float updates, trigArg
-        // (pr is the constant step 2^24) and the repeat test.  When trigArg moves, the sin/cos
-        // and offsets are refreshed (lanes 0/1 sin/cos, lanes 2/3 the offsets) and the pairs of
-        // the batch's remaining steps recomputed.  Half turn h_j = 1/2 [iv_j < 0]: iv's sign bit.
-        const int l = t & 15;
-        const bool off = l == 2 || l == 3;
-        const double C1 = off ? kInv2Pi : kInvPio2;
-        const double Chi = off ? k2PiHi : kPio2Hi;
-        const double Clo = off ? k2PiLo : kPio2Lo;
-        const double Hc = l == 2 ? 0.5 : 0.0;  // lane 2 -B(x, 1/2), lane 3 -B(x, 0)
-        const double* ivs = side + (size_t)s * seg;
-        const int q0 = ctx.q;
-        const float u0 = (q0 & 1) ? p.fbQ : p.fbI, w0 = (q0 & 1) ? p.fbI : -p.fbQ;
-        float fc = (q0 & 2) ? -u0 : u0, nfs = (q0 & 2) ? -w0 : w0;
-        double sn = ctx.sn, cs = ctx.cs;
-        double nB0 = -pll_offset_h(ctx.x, 0.0), nB1 = -pll_offset_h(ctx.x, 0.5);
-        float integ = p.integ, phase = p.phase;
-        uint32_t prev = __builtin_bit_cast(uint32_t, (float)ctx.x);
-        // (Ki e, Kp e) of this lane's step from the current feedback
-        auto ke_of = [&](float vl, double ivl) -> double {
-            const float2v ab = float2v{fc, nfs} * vl;
-            const double Y = fma((double)ab.x, sn, (double)ab.y * cs);
-            const uint64_t ib = __builtin_bit_cast(uint64_t, ivl);
-            const uint64_t m = (uint64_t)(uint32_t)((int)(uint32_t)(ib >> 32) >> 31) * 0x100000001ull;
-            const double nB = __builtin_bit_cast(double, (m & __builtin_bit_cast(uint64_t, nB1)) |
-                                                             (~m & __builtin_bit_cast(uint64_t, nB0)));
-            const float e = (float)fma(Y, ivl, -nB);
-            return __builtin_bit_cast(double, float2v{Ki, Kp} * e);
-        };
-        // fresh feedback and offsets from trigArg a (lanes 0/1 sin/cos, lanes 2/3 the offsets)
-        auto refresh = [&](uint32_t a_bits) {
-            const double xa = (double)__builtin_bit_cast(float, a_bits);
-            const double tq = rint(fma(xa, C1, Hc)) - Hc;
-            const double w = fma(-tq, Clo, fma(-tq, Chi, xa));
-            nB1 = row_bcast<2>(w);
-            nB0 = row_bcast<3>(w);
-            const double W = split_w_horner(w * w, sc);
-            sn = row_bcast<0>(w * W);
-            cs = row_bcast<1>(W);
-            fc = (float)cs;
-            nfs = -(float)sn;
-        };
-        // The repeat test of step j is branched on at step j + 1 (a branch on a compare just
-        // made waits ~40 cycles for it): step j + 1 is computed with the old pairs first and,
-        // when trigArg moved at step j, redone after the refresh.
-        uint64_t moved = 0;
-        // one batch; vb, ivb: this lane's step data (step l of the batch)
-        auto batch = [&](int b, float vb, double ivb) __attribute__((always_inline)) {
-            double ke = ke_of(vb, ivb);
-            float o[NB];
-            unroll_ic(
-                [&](auto jc) {
-                    constexpr int j = decltype(jc)::value;
-                    const float integ0 = integ, phase0 = phase;
-                    const uint32_t prev0 = prev;
-                    uint64_t moved_j;
-                    auto step_j = [&]() {
-                        // the pair as two 32-bit halves (as a float2 the SLP vectorizer pairs
-                        // the adds into packed ops, each read back after a wait state)
-                        const uint64_t kb = __builtin_bit_cast(uint64_t, row_bcast<j>(ke));
-                        integ = integ0 + __builtin_bit_cast(float, (uint32_t)kb);
-                        phase = phase0 + (__builtin_bit_cast(float, (uint32_t)(kb >> 32)) + integ);
-                        const float arg = (float)(prd + (double)phase);
-                        o[j] = arg;
-                        prev = __builtin_bit_cast(uint32_t, arg);
-                        moved_j = __builtin_amdgcn_ballot_w64(prev != prev0);
-                    };
-                    step_j();
-                    if (__builtin_expect(moved != 0, 0)) {  // trigArg moved at step j - 1
-                        refresh(prev0);
-                        ke = ke_of(vb, ivb);
-                        step_j();
-                    }
-                    moved = moved_j;
-                },
-                std::make_integer_sequence<int, NB>{});
-            phase += (inject >= 0 && b == 1 + (inject + s) % (nb - 1)) ? 1.0e-3f : 0.0f;  // test hook
-            float* ob = out + b * NB;
-#pragma unroll
-            for (int q = 0; q < NB / 4; q++)
-                reinterpret_cast<float4*>(ob)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
-            rec[(size_t)s * rb + b] = make_float2(integ, phase);
-        };
-        // The lane's step data is loaded about three batches ahead (a batch here is ~800
-        // cycles, shorter than a load from HBM): ring slot u serves batches 1 + u (mod 4) and is
-        // refilled at the end of its batch, after its last read, so the load lands in place.
-        float vq[4];
-        double ivq[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int bq = 1 + u < nb ? 1 + u : nb - 1;
-            vq[u] = x[bq * NB + l];
-            ivq[u] = ivs[bq * NB + l];
-        }
-        // landed before the loop: the loop top then waits only for the slot it reads (a load
-        // issued last here would make the waitcnt pass wait for every load at each iteration)
-        __builtin_amdgcn_s_waitcnt(0);
-        int b0 = 1;
-        for (; b0 + 3 < nb; b0 += 4) {
-            unroll_ic(
-                [&](auto uc) {
-                    constexpr int u = decltype(uc)::value;
-                    batch(b0 + u, vq[u], ivq[u]);
-                    const int bq = b0 + u + 4 < nb ? b0 + u + 4 : nb - 1;
-                    vq[u] = x[bq * NB + l];
-                    ivq[u] = ivs[bq * NB + l];
-                },
-                std::make_integer_sequence<int, 4>{});
-        }
-        for (; b0 < nb; b0++) batch(b0, x[b0 * NB + l], ivs[b0 * NB + l]);
-        return;
-    }
-    // reduction constants: 2 pi on the offset lanes (lane 2; with SAT lane 3 too), pi/2 on the
-    // sin/cos lanes
-    const bool two_pi = b_lane || (sat && (t & 15) == 3);
-    const double C1 = two_pi ? kInv2Pi : kInvPio2;
-    const double Chi = two_pi ? k2PiHi : kPio2Hi;
-    const double Clo = two_pi ? k2PiLo : kPio2Lo;
-    // half turns: lane 2 reads (h_j, h_j+1), the other lanes the zero pair beside it; with SAT
-    // every lane reads the values (the offset lanes' H is then a constant, see run)
+    // reduction constants: 2 pi on the offset lane (lane 2), pi/2 on the sin/cos lanes
+    const double C1 = b_lane ? kInv2Pi : kInvPio2;
+    const double Chi = b_lane ? k2PiHi : kPio2Hi;
+    const double Clo = b_lane ? k2PiLo : kPio2Lo;
+    // half turns: lane 2 reads (h_j, h_j+1), the other lanes the zero pair beside it
     const double2* shl =
-        reinterpret_cast<const double2*>(side) + seg * (size_t)n_streams + (size_t)s * seg + ((b_lane || sat) ? 0 : 1);
+        reinterpret_cast<const double2*>(side) + seg * (size_t)n_streams + (size_t)s * seg + (b_lane ? 0 : 1);
     float v[NB];
     double iv[NB], pr[NB], hz[NB];
     auto ld_v = [&](int b, int q) {
@@ -690,12 +496,6 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
     double sn = ctx.sn, cs = ctx.cs;
     double nB = -pll_offset_h(ctx.x, iv[0] < 0.0 ? 0.5 : 0.0);
     float integ = p.integ, phase = p.phase;
-    // SAT: the segment starts with trigOffset stuck at 2^24 (filter.cpp:165-166 in float, from
-    // 69.9 s of signal on; pll_side), so trigArg = float(step 2^24 + phase) moves only when
-    // the phase crosses its 0.5 grid -- on ~7.5 % of steps (measured on the bench stream).  With
-    // one stream per wave the test is wave-uniform: a scalar branch skips the sin/cos polynomial,
-    // its broadcasts and conversions (same bits in, same bits out).  The reduction still runs
-    // every step: lane 2's offset B also depends on the next sample's half turn.
     // the rotation's Y = a sn + b cs of a sample from the current feedback (fc, nfs, sn, cs); the
     // one packed op on the chain: one instruction for both products, its wait state often filled
     // by scalar work (measured 0.4 % faster than two v_mul_f32)
@@ -703,107 +503,51 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
         const float2v ab = float2v{fc, nfs} * vv;
         return fma((double)ab.x, sn, (double)ab.y * cs);
     };
-    auto run = [&](auto sat_tag) {
-        constexpr bool SAT = decltype(sat_tag)::value;
-        uint32_t prev = __builtin_bit_cast(uint32_t, (float)ctx.x);  // the trigArg sn, cs belong to
-        // SAT: the offset of the next step depends on x and on that step's half turn only, so
-        // for a repeated trigArg it is one of two values, -B(x, 0) and -B(x, 1/2), refreshed
-        // with sin/cos (lanes 3 and 2, half turns as lane constants) and selected per step.
-        // The next step's Y is formed before the branch on this step's repeat resolves (the
-        // common repeat keeps sn, cs, so Y stands), and again on the rare fresh path.
-        double Yn = 0.0, nB0 = 0.0, nB1 = 0.0;
-        if constexpr (SAT) {
-            Yn = y_of(v[0]);
-            nB0 = -pll_offset_h(ctx.x, 0.0);
-            nB1 = -pll_offset_h(ctx.x, 0.5);
-        }
-        const double Hc = b_lane ? 0.5 : 0.0;  // SAT: lane 2 -B(x, 1/2), lane 3 -B(x, 0)
-        for (int b = 1; b < nb; b++) {
-            const int bn = b + 1 < nb ? b + 1 : b;
-            float o[NB];
+    for (int b = 1; b < nb; b++) {
+        const int bn = b + 1 < nb ? b + 1 : b;
+        float o[NB];
 #pragma unroll
-            for (int j = 0; j < NB; j++) {
-                const double Y = SAT ? Yn : y_of(v[j]);
-                const float e = (float)fma(Y, iv[j], -nB);
-                const float ki_e = Ki * e;
-                const float kp_e = Kp * e;
-                integ = integ + ki_e;
-                phase = phase + (kp_e + integ);
-                const float arg = (float)(pr[j] + (double)phase);
-                o[j] = arg;
-                // sin/cos of r on the sin/cos lanes from the reduction's w
-                auto sincos_step = [&](double w) {
-                    const double z = w * w;
-                    const double W = split_w_horner(z, sc);
-                    sn = row_bcast<0>(w * W);
-                    cs = row_bcast<1>(W);
-                    fc = (float)cs;
-                    nfs = -(float)sn;
-                };
-                if constexpr (SAT) {
-                    const uint32_t ab_bits = __builtin_bit_cast(uint32_t, arg);
-                    const bool changed = __builtin_amdgcn_ballot_w64(ab_bits != prev) != 0;
-                    prev = ab_bits;
-                    // step j + 1's sample: for the last step, the next batch's first (refilled
-                    // at step 3)
-                    const float vn = v[(j + 1) % NB];
-                    Yn = y_of(vn);
-                    asm volatile("" : "+v"(Yn));  // formed here, not sunk past the branch
-                    // unlikely: laid out of line, so the common repeat falls through
-                    if (__builtin_expect(changed, 0)) {
-                        const double xa = (double)arg;
-                        const double tq = rint(fma(xa, C1, Hc)) - Hc;
-                        const double w = fma(-tq, Clo, fma(-tq, Chi, xa));  // r; -B(x, h) on lanes 2, 3
-                        nB1 = row_bcast<2>(w);
-                        nB0 = row_bcast<3>(w);
-                        sincos_step(w);
-                        Yn = y_of(vn);
-                    }
-                    // select by the half turn's bit 29 (set in 0.5's high dword, clear in 0):
-                    // one v_bfe_i32 and two v_bfi_b32, no compare-to-mask wait
-                    const uint64_t hb = __builtin_bit_cast(uint64_t, hz[(j + 1) % NB]);
-                    const uint32_t hi = (uint32_t)(hb >> 32);
-                    // the low dword is unused but still written by its load: keep it live here, or
-                    // the register allocator reuses it and the reuse waits for the load (vmcnt 0)
-                    asm volatile("" ::"v"((uint32_t)hb));
-                    const uint64_t m = (uint64_t)(uint32_t)__builtin_amdgcn_sbfe((int)hi, 29u, 1u) * 0x100000001ull;
-                    nB = __builtin_bit_cast(double, (m & __builtin_bit_cast(uint64_t, nB1)) |
-                                                        (~m & __builtin_bit_cast(uint64_t, nB0)));
-                } else {
-                    const double xa = (double)arg;
-                    const double H = hz[(j + 1) % NB];  // the next step's half turn on lane 2, else 0
-                    const double tq = rint(fma(xa, C1, H)) - H;
-                    const double w = fma(-tq, Clo, fma(-tq, Chi, xa));  // r, or -B on lane 2
-                    nB = row_bcast<2>(w);
-                    sincos_step(w);
-                }
-                // refill after step j: v[j], iv[j], pr[j] and hz[j] (read at step j - 1) are dead
-                if (j % 4 == 3) ld_v(bn, j / 4);
-                if (j % 2 == 1) {
-                    ld_d(iv, siv, bn, j / 2);
-                    ld_d(pr, spr, bn, j / 2);
-                    ld_h(bn, j / 2);
-                }
-                // keep each refill after the step that consumed its registers: hoisted loads
-                // would overlap the old values and cost a register copy per element a batch
-                __builtin_amdgcn_sched_barrier(0);
+        for (int j = 0; j < NB; j++) {
+            const float e = (float)fma(y_of(v[j]), iv[j], -nB);
+            const float ki_e = Ki * e;
+            const float kp_e = Kp * e;
+            integ = integ + ki_e;
+            phase = phase + (kp_e + integ);
+            const float arg = (float)(pr[j] + (double)phase);
+            o[j] = arg;
+            const double xa = (double)arg;
+            const double H = hz[(j + 1) % NB];  // the next step's half turn on lane 2, else 0
+            const double tq = rint(fma(xa, C1, H)) - H;
+            const double w = fma(-tq, Clo, fma(-tq, Chi, xa));  // r, or -B on lane 2
+            nB = row_bcast<2>(w);
+            // sin/cos of r on the sin/cos lanes from the reduction's w
+            const double W = split_w_horner(w * w, sc);
+            sn = row_bcast<0>(w * W);
+            cs = row_bcast<1>(W);
+            fc = (float)cs;
+            nfs = -(float)sn;
+            // refill after step j: v[j], iv[j], pr[j] and hz[j] (read at step j - 1) are dead
+            if (j % 4 == 3) ld_v(bn, j / 4);
+            if (j % 2 == 1) {
+                ld_d(iv, siv, bn, j / 2);
+                ld_d(pr, spr, bn, j / 2);
+                ld_h(bn, j / 2);
             }
-            // test hook (a wrong batch), branch-free
-            phase += (inject >= 0 && b == 1 + (inject + s) % (nb - 1)) ? 1.0e-3f : 0.0f;
-            // every lane stores: the lanes of a row hold the same values, and rows past the last
-            // stream recompute it bit for bit, so the writes agree; with no branch around them
-            // the loads in flight across the loop's back edge need no full wait at its top
-            float* ob = out + b * NB;
-#pragma unroll
-            for (int q = 0; q < NB / 4; q++)
-                reinterpret_cast<float4*>(ob)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
-            rec[(size_t)s * rb + b] = make_float2(integ, phase);
+            // keep each refill after the step that consumed its registers: hoisted loads
+            // would overlap the old values and cost a register copy per element a batch
+            __builtin_amdgcn_sched_barrier(0);
         }
-    };
-    if (sat)
-        run(std::true_type{});
-    else
-        run(std::false_type{});
+        // test hook (a wrong batch), branch-free
+        phase += (inject >= 0 && b == 1 + (inject + s) % (nb - 1)) ? 1.0e-3f : 0.0f;
+        // every lane stores: the lanes of a row hold the same values, and rows past the last
+        // stream recompute it bit for bit, so the writes agree; with no branch around them
+        // the loads in flight across the loop's back edge need no full wait at its top
+        float* ob = out + b * NB;
+#pragma unroll
+        for (int q = 0; q < NB / 4; q++)
+            reinterpret_cast<float4*>(ob)[q] = *reinterpret_cast<const float4*>(&o[4 * q]);
+        rec[(size_t)s * rb + b] = make_float2(integ, phase);
+    }
 }
 
 // One thread per (batch, stream): NB exact steps from the recorded start, compared bit for
@@ -1174,11 +918,10 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         return e ? std::atoi(e) : -1;
     }();
     const bool spec = spec_env && (reinterpret_cast<uintptr_t>(io) & 15) == 0 && stride % 4 == 0;
-    // FMRX_PLL_SAT=0 (measurements, tests): no sin/cos skipping once trigOffset has stuck at 2^24;
-    // =2: the per-step form (cached offsets) instead of the step-parallel one
+    // FMRX_PLL_SAT=0 (measurements, tests): saturated segments on the ordinary runner too
     const int sat_ok = [] {
         const char* e = std::getenv("FMRX_PLL_SAT");
-        return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
+        return (e && e[0] == '0') ? 0 : 1;
     }();
     int spw = 1;
     while (spw < 64 && (long long)spw * n_simd < n_streams) spw *= 2;
@@ -1202,10 +945,14 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         float* out = spec ? args : x;
         const size_t ostride = spec ? seg : stride;
         if (spec) {
-            if (spw <= 4)
+            if (spw <= 4) {
                 hipLaunchKernelGGL(pll_spec_lane_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw, stride,
                                    side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject, sat_ok);
-            else
+                // saturated streams (pll_sat_segment), which the lane kernel leaves to it
+                if (sat_ok && spw == 1)
+                    launch_pll_sat(grid, block, s, x, m, n_streams, spw, stride, side, seg, step, norm_bw, st, args,
+                                   seg, fail, rec, rb, inject);
+            } else
                 hipLaunchKernelGGL(pll_spec_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw,
                                    stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
             const int nb = m / kPllBatch;

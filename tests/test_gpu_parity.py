@@ -516,11 +516,11 @@ def test_pll_primitive_states(fmrx, orc, trig, phase, freq, fs, n, offset):
 
 @pytest.mark.parametrize("freq,nco_scale", [(19000, 2.0), (114000, 0.5)])  # pilot (project.cpp:166), RDS (:226)
 @pytest.mark.parametrize("inject", [None, "3"])
-@pytest.mark.parametrize("sat", ["1", "2", "0"])
+@pytest.mark.parametrize("sat", ["1", "0"])
 def test_pll_saturated_runner(fmrx, orc, monkeypatch, inject, sat, freq, nco_scale):
     """A segment that starts with trigOffset stuck at 2^24 (filter.cpp:165-166 in float, 69.9 s
-    into a stream): the speculative runner's saturated forms (1 step-parallel, 2 per-step with
-    cached offsets, 0 none), and a corrupted runner batch (check + certified resume).  The
+    into a stream): the saturated-segment runner (pll_sat.hip; FMRX_PLL_SAT=0: the ordinary
+    one), and a corrupted runner batch (check + certified resume).  The
     speculation counters must show every batch verified without the corruption -- a runner
     that disagrees with the exact path would otherwise pass here, fixed up by the resume."""
     monkeypatch.setenv("FMRX_PLL_SAT", sat)
