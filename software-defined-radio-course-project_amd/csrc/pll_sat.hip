@@ -99,9 +99,7 @@ __global__ void __launch_bounds__(256) pll_sat_kernel(const float* io, int n, in
         fc = (float)cs;
         nfs = -(float)sn;
     };
-    // The repeat test of step j is branched on at step j + 1 (a branch on a compare just
-    // made waits ~40 cycles for it): step j + 1 is computed with the old pairs first and,
-    // when trigArg moved at step j, redone after the refresh.
+    // the moved flag of the last step computed, tested with the next pair (see below)
     uint64_t moved = 0;
     // one batch; vb, ivb: this lane's step data (step l of the batch)
     auto batch = [&](int b, float vb, double ivb) __attribute__((always_inline)) {
