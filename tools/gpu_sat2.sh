@@ -1,6 +1,8 @@
 #!/bin/bash
 # Step-parallel saturated runner (FMRX_PLL_SAT=1) vs the per-step form (2): PLL runner tests
-# with the speculation counters, then configs[2] (1 GiB stereo) under each form.
+# with the speculation counters, then configs[2] (1 GiB stereo) under each form.  (Kept as the
+# recipe of profiles/r02/sat/gib_*; the per-step form was removed after this A/B, so today both
+# values select pll_sat_kernel.)
 set -o pipefail
 OUT=gpurun_out/${1:-sat2}
 mkdir -p $OUT
