@@ -16,5 +16,5 @@ for v in $VARIANTS; do
         python3 tools/bench_stereo.py --streams $ns > $OUT/kt_${v}_$ns.log 2>&1 || exit 3
   done
 done
-cp $PKG/libfmrx_noslp.so $PKG/libfmrx.so
+cp $PKG/libfmrx_${VARIANTS%% *}.so $PKG/libfmrx.so  # the first variant back in place
 echo done
