@@ -436,6 +436,23 @@ def test_stereo_long_hash(fmrx, name):
         assert sha(rx.process(iq)) == h["pcm_sha256"]
 
 
+def test_stereo_long_hash_three_streams(fmrx):
+    """The saturated-segment runner (pll_sat.hip) with several waves: three copies of the 72 s
+    long run in one 3-stream call, each stream's PCM against the reference build's hash."""
+    h = long_runs()["m0_rf51_synth_72s"]
+    bb, rf_fs = oracle.MODES[h["mode"]][0], oracle.MODES[h["mode"]][3]
+    iq = iqgen.make(h["recipe"], h["n_blocks"] * bb, rf_fs)
+    with fmrx.Receiver(h["mode"], fmrx.STEREO, rf_taps=h["rf_taps"], n_streams=3) as rx:
+        counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+        rx.debug_pll_stats(counts.data_ptr())
+        out = rx.process(np.stack([iq, iq, iq]))
+        rx.debug_pll_stats(None)
+    for s in range(3):
+        assert sha(out[s]) == h["pcm_sha256"], s
+    resumed, checked = counts.cpu().tolist()
+    assert checked > 0 and resumed <= checked // 10000, (resumed, checked)
+
+
 @pytest.mark.parametrize("name", [n for n in long_runs() if long_runs()[n]["mode"] in (2, 3)])
 def test_polyphase_mono_long_hash(fmrx, name):
     h = long_runs()[name]
