@@ -453,6 +453,48 @@ def test_stereo_long_hash_three_streams(fmrx):
     assert checked > 0 and resumed <= checked // 10000, (resumed, checked)
 
 
+def _stream_blob(multi: bytes, single_hdr: bytes, ns: int, s: int) -> bytes:
+    """Stream s's slice of an n_streams state blob, as a 1-stream blob (api.cpp state_io order:
+    halo, audio history, demod history, PLL, mixer tail, mono state)."""
+    hdr = np.frombuffer(multi[:40], np.uint32)
+    sizes = [int(hdr[6]), 4 * int(hdr[7]), 4 * 64, 4 * 8, 4 * 64, 4 * 8]
+    out, off = [single_hdr[:40]], 40
+    for z in sizes:
+        out.append(multi[off + s * z: off + (s + 1) * z])
+        off += ns * z
+    assert off == len(multi)
+    return b"".join(out)
+
+
+def test_saturated_runner_wide_grid(fmrx):
+    """pll_sat.hip on a grid of 4-wave workgroups (300 streams, one a wave): every stream's PLL
+    is put at trigOffset 2^24 through the state blob, 40 blocks run in one call, and streams
+    across the workgroups are compared with the same stream alone in a 1-stream context (whose
+    saturated runner the long-run hashes pin to the reference build)."""
+    ns, nb, bb = 300, 40, 12800
+    ins = np.stack([iqgen.make("synth:%d" % (600 + s % 7), (nb + 2) * bb) for s in range(ns)])
+    with fmrx.Receiver(0, fmrx.STEREO, n_streams=ns) as rx:
+        rx.process(ins[:, : 2 * bb])  # a state to start from
+        blob = bytearray(rx.get_state())
+        hdr = np.frombuffer(bytes(blob[:40]), np.uint32)
+        pll_off = 40 + ns * (int(hdr[6]) + 4 * int(hdr[7]) + 4 * 64)
+        pll = np.frombuffer(bytes(blob[pll_off: pll_off + ns * 32]), np.float32).reshape(ns, 8).copy()
+        pll[:, 5] = 16777216.0
+        blob[pll_off: pll_off + ns * 32] = pll.tobytes()
+        rx.set_state(bytes(blob))
+        counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+        rx.debug_pll_stats(counts.data_ptr())
+        out = rx.process(ins[:, 2 * bb:])
+        rx.debug_pll_stats(None)
+    resumed, checked = counts.cpu().tolist()
+    assert checked > 0 and resumed == 0, (resumed, checked)
+    for s in (0, 1, 63, 64, 255, 256, 299):
+        with fmrx.Receiver(0, fmrx.STEREO) as r1:
+            r1.process(ins[s, : 2 * bb])
+            r1.set_state(_stream_blob(bytes(blob), r1.get_state(), ns, s))
+            assert np.array_equal(r1.process(ins[s, 2 * bb:]), out[s]), s
+
+
 @pytest.mark.parametrize("name", [n for n in long_runs() if long_runs()[n]["mode"] in (2, 3)])
 def test_polyphase_mono_long_hash(fmrx, name):
     h = long_runs()[name]
