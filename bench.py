@@ -328,6 +328,7 @@ def other_configs(fmrx) -> dict:
         out["configs[2]"] = {"workload": f"mode-0 stereo (REF_EXACT), one stream, 1 GiB ({nb} blocks) in one call",
                              "seconds": round(dt, 3), "MS_per_s": round(nb * bb / 2 / dt / 1e6, 1),
                              "x_realtime": round(sig / dt, 1)}
+        out["configs[2]"].update(parity_vs_reference("bench_c2_m0_stereo_gib", iq, pcm))
         rx.close()
         del iq, pcm
         torch.cuda.empty_cache()
@@ -347,10 +348,31 @@ def other_configs(fmrx) -> dict:
         out["configs[3]"] = {"workload": f"mode-2 mono, 147/800 polyphase resampler, 1 GiB ({nb} blocks)",
                              "ms_per_step": round(dt * 1e3, 4), "MS_per_s": round(nb * bb / 2 / dt / 1e6, 1),
                              "x_realtime": round(nb * bb / 2 / rx.geo.rf_fs / dt, 1)}
+        # the timed steps carried state from step to step: the parity pass starts fresh
+        rx.reset()
+        rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
+        rx.synchronize()
+        out["configs[3]"].update(parity_vs_reference("bench_c3_m2_mono_gib", iq, pcm))
         rx.close()
     except Exception as e:  # the headline line must still print
         out["error"] = repr(e)
     return out
+
+
+def parity_vs_reference(key: str, d_iq, d_pcm) -> dict:
+    """Full-size parity of an extra config, after its timing: SHA-256 of the bench's input and
+    of the GPU's PCM against the reference build's over the same bytes (tests/golden/hashes.json
+    `bench_*`, written by tests/golden/make_golden.py --bench-only through oracle/_ref)."""
+    import hashlib
+
+    with open(os.path.join(REPO, "tests", "golden", "hashes.json")) as f:
+        want = json.load(f)[key]
+    got_in = hashlib.sha256(d_iq.cpu().numpy().tobytes()).hexdigest()
+    got_pcm = hashlib.sha256(d_pcm.cpu().numpy().tobytes()).hexdigest()
+    return {"input_matches_fixture": got_in == want["input_sha256"],
+            "bit_exact_vs_reference": got_in == want["input_sha256"] and got_pcm == want["pcm_sha256"],
+            "parity_source": f"tests/golden/hashes.json {key}: reference build (oracle/_ref) "
+                             f"{want['field']} SHA-256 over the same {want['n_blocks']} blocks"}
 
 
 def cpu_baseline(d_iq, d_pcm, sample_bytes, bb, na):

@@ -185,13 +185,13 @@ int16_t orc_quant(float x) {
 }
 
 /* Sequential src/project.cpp (rf_thread :48-84 then audio_thread :132-196 per block; all
- * full blocks, no EOF race) plus the private-history mono product.  Returns blocks done. */
-long orc_run(int mode, int rf_taps, const uint8_t* iq, size_t nbytes, orc_outputs* o) {
-    orc_mode m;
-    if (orc_geometry(mode, &m) != 0 || rf_taps < 2) return -1;
+ * full blocks, no EOF race) plus the private-history mono product.  With demod_in set, the
+ * rf_thread half is skipped and block b's demod is demod_in + b * if_samples. */
+static long run_blocks(const orc_mode* mp, int rf_taps, const uint8_t* iq, const float* demod_in,
+                       long n_blocks, orc_outputs* o) {
+    const orc_mode m = *mp;
     const int bp_taps = 51, mono_delay = 5;
     const int B = m.block_bytes, H = B / 2, NIF = m.if_samples, NA = m.audio_frames;
-    const long n_blocks = (long)(nbytes / (size_t)B);
     const int at = m.audio_taps;
 
     float* rf_c = malloc(sizeof(float) * rf_taps);
@@ -229,14 +229,18 @@ long orc_run(int mode, int rf_taps, const uint8_t* iq, size_t nbytes, orc_output
     float pll[6] = {0.0f, 0.0f, 1.0f, 0.0f, 1.0f, 0.0f}; /* project.cpp:106-111 */
 
     for (long b = 0; b < n_blocks; b++) {
-        orc_normalize(iq + (size_t)b * B, B, xb);
-        for (int k = 0; k < H; k++) {
-            ib[k] = xb[2 * k];
-            qb[k] = xb[2 * k + 1];
+        if (demod_in) {
+            memcpy(dem, demod_in + (size_t)b * NIF, sizeof(float) * NIF);
+        } else {
+            orc_normalize(iq + (size_t)b * B, B, xb);
+            for (int k = 0; k < H; k++) {
+                ib[k] = xb[2 * k];
+                qb[k] = xb[2 * k + 1];
+            }
+            orc_resample(ids, st_i, ib, H, rf_c, rf_taps, 1, m.rf_decim);
+            orc_resample(qds, st_q, qb, H, rf_c, rf_taps, 1, m.rf_decim);
+            orc_fmdemod(dem, prev, ids, qds, NIF);
         }
-        orc_resample(ids, st_i, ib, H, rf_c, rf_taps, 1, m.rf_decim);
-        orc_resample(qds, st_q, qb, H, rf_c, rf_taps, 1, m.rf_decim);
-        orc_fmdemod(dem, prev, ids, qds, NIF);
         if (o->demod) memcpy(o->demod + b * NIF, dem, sizeof(float) * NIF);
 
         orc_resample(mind, st_in, dem, NIF, au_c, at, m.audio_interp, m.audio_decim);
@@ -276,6 +280,19 @@ long orc_run(int mode, int rf_taps, const uint8_t* iq, size_t nbytes, orc_output
     free(shift); free(left); free(right); free(st_i); free(st_q); free(st_ch); free(st_ca);
     free(st_au); free(st_in);
     return n_blocks;
+}
+
+long orc_run(int mode, int rf_taps, const uint8_t* iq, size_t nbytes, orc_outputs* o) {
+    orc_mode m;
+    if (orc_geometry(mode, &m) != 0 || rf_taps < 2) return -1;
+    return run_blocks(&m, rf_taps, iq, NULL, (long)(nbytes / (size_t)m.block_bytes), o);
+}
+
+/* audio_thread alone (project.cpp:132-196) over n_blocks demod blocks of if_samples floats. */
+long orc_run_audio(int mode, const float* demod, size_t n_blocks, orc_outputs* o) {
+    orc_mode m;
+    if (orc_geometry(mode, &m) != 0) return -1;
+    return run_blocks(&m, 51, NULL, demod, (long)n_blocks, o);
 }
 
 /* RDS front half, the rds_thread body (src/project.cpp:200-271, dead code in the reference):

@@ -50,6 +50,7 @@ int orc_mixer(float* out, const float* a, const float* b, int n);
 int orc_lr(float* left, float* right, const float* mono, const float* stereo, int n);
 int16_t orc_quant(float x);
 long orc_run(int mode, int rf_taps, const uint8_t* iq, size_t nbytes, orc_outputs* o);
+long orc_run_audio(int mode, const float* demod, size_t n_blocks, orc_outputs* o);
 int orc_fm_demod_arctan(double* out, double* prev_phase, const double* i_in, const double* q_in, int n);
 int orc_estimate_psd(const float* samples, size_t n, int freq_bins, float fs, float* freq, float* psd);
 long orc_rds(int mode, const float* demod, size_t n_blocks, float* channel, float* carrier,

@@ -76,10 +76,14 @@ class _Lib:
             raise FileNotFoundError(f"{self.path} not built (run oracle.build())")
         self.lib = C.CDLL(self.path)
 
-    def _run(self, fn, mode: int, rf_taps: int, iq, fields=None) -> dict:
-        iq = _as_u8(iq)
+    def _run(self, fn, mode: int, rf_taps: int, iq, fields=None, demod=None) -> dict:
         bb, nif, na = MODES[mode][:3]
-        nb = iq.size // bb
+        if demod is not None:  # audio stage only: demod blocks in
+            demod = np.ascontiguousarray(demod, np.float32)
+            nb = demod.size // nif
+        else:
+            iq = _as_u8(iq)
+            nb = iq.size // bb
         fields = fields or FIELDS
         arrays = {}
         o = Outputs()
@@ -99,12 +103,21 @@ class _Lib:
             arrays[f] = a
             setattr(o, f, _ptr(a, _i16p if a.dtype == np.int16 else _fp))
         fn.restype = C.c_long
-        fn.argtypes = [C.c_int, C.c_int, _u8p, C.c_size_t, C.POINTER(Outputs)]
-        n = fn(mode, rf_taps, _ptr(iq, _u8p), iq.size, C.byref(o))
+        if demod is not None:
+            fn.argtypes = [C.c_int, _fp, C.c_size_t, C.POINTER(Outputs)]
+            n = fn(mode, _ptr(demod, _fp), nb, C.byref(o))
+        else:
+            fn.argtypes = [C.c_int, C.c_int, _u8p, C.c_size_t, C.POINTER(Outputs)]
+            n = fn(mode, rf_taps, _ptr(iq, _u8p), iq.size, C.byref(o))
         if n < 0:
             raise ValueError("bad mode")
         arrays["n_blocks"] = n
         return arrays
+
+    def run_audio(self, mode: int, demod, fields=None) -> dict:
+        """audio_thread alone (project.cpp:132-196) over whole demod blocks (if_samples each),
+        plus the private-history mono product; the same output fields as run()."""
+        return self._run(getattr(self.lib, self.prefix + "run_audio"), mode, 51, None, fields, demod)
 
     def lpf(self, fs, fc, taps, gain=1):
         h = np.zeros(taps, np.float32)

@@ -170,56 +170,31 @@ int ref_normalize(const uint8_t* bytes, int n, float* out) {
     return n;
 }
 
-// Sequential project.cpp (all full blocks) + the private-state mono product.
-// Returns the number of blocks processed, or -1 on a bad mode.
-long ref_run(int mode, int rf_taps, const uint8_t* iq, size_t nbytes, ref_outputs* o) {
+// audio_thread locals (project.cpp:93-130) and body (:143-195) for one demod block, plus the
+// private-state mono product (the mono resample of :146 with its own history vector).
+struct AudioStage {
     RefMode m;
-    if (!ref_mode(mode, &m)) return -1;
-    const int rf_fc = 100000, audio_fc = 16000, bp_taps = 51, mono_delay = 5;  // :304-308
-    const int block_size = 256 * m.rf_decim * m.audio_decim;                     // :364
-    const long n_blocks = (long)(nbytes / (size_t)block_size);
-    CinRedirect cin_from(iq, nbytes);
-
-    // ---- rf_thread locals (project.cpp:26-46)
-    std::vector<float> iq_block(block_size);
-    const int half = int(iq_block.size() * 0.5);
-    std::vector<float> i_block(half), q_block(half);
-    std::vector<float> state_i(rf_taps - 1, 0.0), state_q(rf_taps - 1, 0.0);
-    std::vector<float> rf_coeff;
-    impulseResponseLPF(rf_coeff, m.rf_fs, rf_fc, rf_taps, 1);
-    std::vector<float> i_ds, q_ds, demod;
-    float prev_i = 0.0, prev_q = 0.0;
-
-    // ---- audio_thread locals (project.cpp:93-130)
-    std::vector<float> channel, channel_state(bp_taps - 1, 0.0), channel_coeff;
-    impulseResponseBPF(channel_coeff, m.bp_fs, 22000.0, 54000.0, bp_taps);
-    std::vector<float> carrier, carrier_state(bp_taps - 1, 0.0), carrier_coeff;
-    impulseResponseBPF(carrier_coeff, m.bp_fs, 18500, 19500, bp_taps);
+    const int audio_fc = 16000, bp_taps = 51, mono_delay = 5;  // project.cpp:304-308
+    std::vector<float> channel, channel_state, channel_coeff;
+    std::vector<float> carrier, carrier_state, carrier_coeff;
     float integrator = 0.0, phaseEst = 0.0, feedbackI = 1.0, feedbackQ = 0.0, trigOffset = 0.0,
           ncoOut_state = 1.0;
-    std::vector<float> audio_state(m.audio_taps - 1, 0.0), audio_coeff;
-    impulseResponseLPF(audio_coeff, m.if_fs, audio_fc, m.audio_taps, m.audio_interp);
-    std::vector<float> mono_shift, mono, mono_state(mono_delay, 0.0);
+    std::vector<float> audio_state, audio_coeff;
+    std::vector<float> mono_shift, mono, mono_state;
     std::vector<float> mixer_v, left, right, stereo;
-    std::vector<short> audio;
-    // private-state mono product
-    std::vector<float> indep_state(m.audio_taps - 1, 0.0), mono_indep;
+    std::vector<float> indep_state, mono_indep;
 
-    for (long b = 0; b < n_blocks; b++) {
-        readStdinBlockData(block_size, (unsigned)b, iq_block);
-        int j = 0;
-        for (int i = 0; i < (int)iq_block.size(); i += 2) {
-            i_block[j] = iq_block[i];
-            q_block[j] = iq_block[i + 1];
-            j++;
-        }
-        resample(i_ds, state_i, i_block, rf_coeff, 1, m.rf_decim);
-        resample(q_ds, state_q, q_block, rf_coeff, 1, m.rf_decim);
-        FMDemod(demod, prev_i, prev_q, i_ds, q_ds);
+    explicit AudioStage(const RefMode& mm)
+        : m(mm), channel_state(bp_taps - 1, 0.0), carrier_state(bp_taps - 1, 0.0),
+          audio_state(mm.audio_taps - 1, 0.0), mono_state(mono_delay, 0.0),
+          indep_state(mm.audio_taps - 1, 0.0) {
+        impulseResponseBPF(channel_coeff, m.bp_fs, 22000.0, 54000.0, bp_taps);
+        impulseResponseBPF(carrier_coeff, m.bp_fs, 18500, 19500, bp_taps);
+        impulseResponseLPF(audio_coeff, m.if_fs, audio_fc, m.audio_taps, m.audio_interp);
+    }
 
+    void block(const std::vector<float>& demod, long b, ref_outputs* o) {
         const size_t nif = demod.size();
-        put(o->demod, b * nif, demod);
-
         // mono product with its own history
         resample(mono_indep, indep_state, demod, audio_coeff, m.audio_interp, m.audio_decim);
         const size_t na = mono_indep.size();
@@ -262,7 +237,58 @@ long ref_run(int mode, int rf_taps, const uint8_t* iq, size_t nbytes, ref_output
             }
         }
     }
+};
+
+// Sequential project.cpp (all full blocks) + the private-state mono product.
+// Returns the number of blocks processed, or -1 on a bad mode.
+long ref_run(int mode, int rf_taps, const uint8_t* iq, size_t nbytes, ref_outputs* o) {
+    RefMode m;
+    if (!ref_mode(mode, &m)) return -1;
+    const int rf_fc = 100000;                                  // project.cpp:304
+    const int block_size = 256 * m.rf_decim * m.audio_decim;  // :364
+    const long n_blocks = (long)(nbytes / (size_t)block_size);
+    CinRedirect cin_from(iq, nbytes);
+
+    // ---- rf_thread locals (project.cpp:26-46)
+    std::vector<float> iq_block(block_size);
+    const int half = int(iq_block.size() * 0.5);
+    std::vector<float> i_block(half), q_block(half);
+    std::vector<float> state_i(rf_taps - 1, 0.0), state_q(rf_taps - 1, 0.0);
+    std::vector<float> rf_coeff;
+    impulseResponseLPF(rf_coeff, m.rf_fs, rf_fc, rf_taps, 1);
+    std::vector<float> i_ds, q_ds, demod;
+    float prev_i = 0.0, prev_q = 0.0;
+    AudioStage audio(m);
+
+    for (long b = 0; b < n_blocks; b++) {
+        readStdinBlockData(block_size, (unsigned)b, iq_block);
+        int j = 0;
+        for (int i = 0; i < (int)iq_block.size(); i += 2) {
+            i_block[j] = iq_block[i];
+            q_block[j] = iq_block[i + 1];
+            j++;
+        }
+        resample(i_ds, state_i, i_block, rf_coeff, 1, m.rf_decim);
+        resample(q_ds, state_q, q_block, rf_coeff, 1, m.rf_decim);
+        FMDemod(demod, prev_i, prev_q, i_ds, q_ds);
+        put(o->demod, b * demod.size(), demod);
+        audio.block(demod, b, o);
+    }
     return n_blocks;
+}
+
+// audio_thread alone (project.cpp:132-196) over given demod blocks (if_samples floats each),
+// e.g. the reference's own data/fm_demod_10.bin; o->demod is ignored.  Returns the blocks run.
+long ref_run_audio(int mode, const float* demod, size_t n_blocks, ref_outputs* o) {
+    RefMode m;
+    if (!ref_mode(mode, &m)) return -1;
+    const size_t nif = (size_t)(256 * m.rf_decim * m.audio_decim) / 2 / m.rf_decim;
+    AudioStage audio(m);
+    for (size_t b = 0; b < n_blocks; b++) {
+        std::vector<float> d(demod + b * nif, demod + (b + 1) * nif);
+        audio.block(d, (long)b, o);
+    }
+    return (long)n_blocks;
 }
 
 // CPU baseline: the reference's sequential mono-only receive path (rf_thread body +

@@ -80,11 +80,21 @@ def case_input(z):
     return iqgen.make(z["recipe"], z["n_blocks"] * bb, rf_fs)
 
 
-def long_runs():
+def _hashes():
     with open(os.path.join(GOLDEN, "hashes.json")) as f:
         h = json.load(f)
     h.pop("meta")
     return h
+
+
+def long_runs():
+    """Long-run hashes (2-100 s of signal): pcm, pcm_mono and the last PLL state."""
+    return {k: v for k, v in _hashes().items() if not k.startswith("bench_")}
+
+
+def bench_runs():
+    """Hashes of the reference PCM over exactly bench.py's 1 GiB inputs (configs[2], [3])."""
+    return {k: v for k, v in _hashes().items() if k.startswith("bench_")}
 
 
 def has_gpu() -> bool:

@@ -35,6 +35,11 @@ def test_bench_json_contract():
     oc = j["baseline_configs"]  # the other single-GPU BASELINE configs, same box
     assert "error" not in oc, oc
     assert oc["configs[2]"]["x_realtime"] > 1 and oc["configs[3]"]["MS_per_s"] > 0
+    # full-size parity of both extra configs against the reference build's PCM hashes of the
+    # same bytes (tests/golden/hashes.json bench_*): /root/reference/src/project.cpp:132-196
+    for c in ("configs[2]", "configs[3]"):
+        assert oc[c]["input_matches_fixture"] is True, oc[c]
+        assert oc[c]["bit_exact_vs_reference"] is True, oc[c]
     rf = j["roofline"]
     assert rf["bound"] in ("hbm", "mfma") and rf["unit"] in ("GB/s", "TFLOP/s")
     assert 0 < rf["frac"] < 1 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3

@@ -16,7 +16,7 @@ import pytest
 
 import iqgen
 import oracle
-from conftest import case_input, golden_cases, load_case, long_runs
+from conftest import bench_runs, case_input, golden_cases, load_case, long_runs
 
 pytestmark = pytest.mark.gpu
 
@@ -203,6 +203,58 @@ def test_thread_split_block_by_block(fmrx, orc, mode, nb):
     with fmrx.Receiver(mode, fmrx.STEREO) as rx:
         got = [rx.audio_block(rx.rf_block(iq[b * bb:(b + 1) * bb])) for b in range(nb)]
     assert np.array_equal(np.concatenate(got), orc.run(mode, 51, iq, ["pcm"])["pcm"])
+
+
+@pytest.mark.parametrize("channels", [2, 1])
+def test_two_context_thread_split_overlaps(fmrx, orc, channels):
+    """INTEGRATION.md Option 1 in its overlapping form: project.cpp's two threads, each with
+    its OWN context -- context A only runs fmrx_rf_block (it owns the RF histories and the
+    demodulator's previous sample), context B only fmrx_audio_block (the band-pass histories,
+    PLL, shared audio_state and mono delay) -- joined by a bounded queue of depth 3
+    (QUEUE_CAPACITY, project.cpp:17,71-80,133-141).  48 blocks one per call: B's PCM equals
+    the oracle's, and the stages really ran concurrently (ctypes drops the GIL; each context
+    has its own lock)."""
+    import queue
+    import threading
+    import time
+
+    nb, bb = 48, 12800
+    iq = iqgen.make("synth:63", nb * bb)
+    q = queue.Queue(maxsize=3)
+    spans = {"rf": [], "audio": []}
+    out, errors = [], []
+    with fmrx.Receiver(0, channels) as ra, fmrx.Receiver(0, channels) as rb:
+        def rf_thread():
+            try:
+                for b in range(nb):
+                    t0 = time.perf_counter()
+                    d = ra.rf_block(iq[b * bb:(b + 1) * bb])
+                    spans["rf"].append((t0, time.perf_counter()))
+                    q.put(d)
+            except Exception as e:  # pragma: no cover - surfaced below
+                errors.append(e)
+            q.put(None)
+
+        def audio_thread():
+            try:
+                while (d := q.get()) is not None:
+                    t0 = time.perf_counter()
+                    out.append(rb.audio_block(d))
+                    spans["audio"].append((t0, time.perf_counter()))
+            except Exception as e:  # pragma: no cover
+                errors.append(e)
+
+        ts = [threading.Thread(target=rf_thread), threading.Thread(target=audio_thread)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+    assert not errors, errors
+    field = "pcm" if channels == 2 else "pcm_mono"
+    assert len(out) == nb
+    assert np.array_equal(np.concatenate(out), orc.run(0, 51, iq, [field])[field])
+    overlapped = sum(1 for a0, a1 in spans["audio"] for r0, r1 in spans["rf"] if r0 < a1 and a0 < r1)
+    assert overlapped >= nb // 4, overlapped
 
 
 def test_mono_multistream_independent(fmrx, orc):
@@ -502,6 +554,26 @@ def test_polyphase_mono_long_hash(fmrx, name):
     iq = iqgen.make(h["recipe"], h["n_blocks"] * bb, rf_fs)
     with fmrx.Receiver(h["mode"], fmrx.MONO, rf_taps=h["rf_taps"]) as rx:
         assert sha(rx.process(iq)) == h["pcm_mono_sha256"]
+
+
+@pytest.mark.parametrize("name", sorted(bench_runs()))
+def test_bench_config_full_size_hash(fmrx, name):
+    """BASELINE configs[2] (mode-0 stereo, ONE 1 GiB stream: 223.7 s of signal, two thirds of
+    it past the PLL's trigOffset saturation, project.cpp:132-196 / filter.cpp:136-174) and
+    configs[3] (mode-2 mono, 1 GiB) at full size on exactly bench.py's device-generated input,
+    against the reference build's PCM hash of the same bytes."""
+    h = bench_runs()[name]
+    bb = oracle.MODES[h["mode"]][0]
+    nb = h["n_blocks"]
+    with fmrx.Receiver(h["mode"], h["channels"], rf_taps=h["rf_taps"]) as rx:
+        d_iq = torch.empty(nb * bb, dtype=torch.uint8, device="cuda")
+        d_pcm = torch.empty(nb * rx.geo.pcm_samples, dtype=torch.int16, device="cuda")
+        torch.cuda.synchronize()
+        rx.synth_device(int(h["recipe"][6:]), 0, nb * bb // 2, d_iq.data_ptr())
+        rx.process_device(d_iq.data_ptr(), nb, d_pcm.data_ptr())
+        rx.synchronize()
+        assert sha(d_iq.cpu().numpy()) == h["input_sha256"]
+        assert sha(d_pcm.cpu().numpy()) == h["pcm_sha256"], name
 
 
 # ---- filter.h primitives --------------------------------------------------------------------
