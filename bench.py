@@ -147,7 +147,10 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-bytes", type=int, default=STREAM_BYTES)
     ap.add_argument("--no-other-configs", action="store_true",
-                    help="skip the extra BASELINE configs (stereo 1 GiB, mode-2 mono) timed at N=1")
+                    help="skip the extra BASELINE configs (stereo 1 GiB, mode-2 mono at N=1; the 256-stream "
+                         "stereo configs[4] at every N)")
+    ap.add_argument("--streams-seconds", type=float, default=60.0,
+                    help="configs[4] stream length (256 stereo streams sharded over the ranks)")
     args = ap.parse_args()
 
     import numpy as np
@@ -291,10 +294,14 @@ def main() -> None:
         line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(d_iq, args.cpu_sample_bytes, bb, host["usable_cores"])
         if line["cpu_baseline_all_cores"] is not None:
             line["cpu_baseline_all_cores"]["host"] = host
-    if world == 1 and not args.no_other_configs:
+    if not args.no_other_configs:
         del d_iq, d_pcm
+        rx.close()
         torch.cuda.empty_cache()
-        line["baseline_configs"] = other_configs(fmrx)
+        line["baseline_configs"] = other_configs(fmrx) if world == 1 else {}
+        c4 = streams_config(fmrx, world, rank, dev if world > 1 else 0, args.streams_seconds)
+        if rank == 0:
+            line["baseline_configs"]["configs[4]"] = c4
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
@@ -373,6 +380,26 @@ def parity_vs_reference(key: str, d_iq, d_pcm) -> dict:
             "bit_exact_vs_reference": got_in == want["input_sha256"] and got_pcm == want["pcm_sha256"],
             "parity_source": f"tests/golden/hashes.json {key}: reference build (oracle/_ref) "
                              f"{want['field']} SHA-256 over the same {want['n_blocks']} blocks"}
+
+
+def streams_config(fmrx, world: int, rank: int, dev: int, seconds: float) -> dict | None:
+    """BASELINE configs[4] at this N (extra key; `value` stays configs[1]): 256 independent
+    mode-0 stereo streams of `seconds` each, sharded contiguously over the ranks (one process per
+    GPU), each rank's shard one device-resident multi-stream call, the S16 PCM gathered to rank 0
+    over RCCL (dist.streams_leg); max-over-ranks time of processing + gather.  Rank 0 checks
+    streams 0, 127, 128, 255 of the gathered PCM against the reference build's hashes
+    (tests/golden/hashes.json streams_c4_60s; other lengths: the streams recorded for them)."""
+    import iqgen
+    import torch
+
+    dmod = iqgen.load_module("dist")
+    expect = iqgen.stream_hashes(256, int(seconds * RT_RATE * 2 // 12800)) or None
+    try:
+        res = dmod.streams_leg(fmrx, 256, seconds, world, rank, dev, expect=expect)
+    except Exception as e:  # the headline line must still print
+        res = {"error": repr(e)} if rank == 0 else None
+    torch.cuda.empty_cache()
+    return res
 
 
 def cpu_baseline(d_iq, d_pcm, sample_bytes, bb, na):

@@ -185,6 +185,11 @@ int fmrx_psd_device(fmrx_ctx* ctx, const float* d_samples, size_t n, int freq_bi
 int fmrx_synth_host(uint64_t seed, int rf_fs, uint64_t first_pair, size_t n_pairs, uint8_t* out);
 int fmrx_synth_device(fmrx_ctx* ctx, uint64_t seed, int rf_fs, uint64_t first_pair,
                       size_t n_pairs, uint8_t* d_out);
+/* n_seeds streams in ONE launch: stream k (seed seeds[k], host array) is written at
+ * d_out + k * stride_bytes, samples [first_pair, first_pair + n_pairs) each (stride_bytes even
+ * and >= 2 n_pairs).  Returns after the launch has completed (the seed table is uploaded).    */
+int fmrx_synth_device_streams(fmrx_ctx* ctx, const uint64_t* seeds, size_t n_seeds, int rf_fs,
+                              uint64_t first_pair, size_t n_pairs, uint8_t* d_out, size_t stride_bytes);
 
 /* ---- test hook: the PLL's fallback libm (src/filter.cpp:161,168-170 on refused args) ---- */
 /* Runs the device functions the PLL calls where its certified fast paths refuse, on device

@@ -112,6 +112,7 @@ struct fmrx_ctx {
     DevBuf<float> d_scratch;
     DevBuf<double> d_pll_side;    // PLL side data of one segment (pll_side_doubles)
     DevBuf<int16_t> d_sintab;
+    DevBuf<uint8_t> d_synth_params;  // fmrx_synth_device_streams: SynthParams per stream
     // kernel timing: pairs of HIP events recorded around each fused-kernel launch on the
     // context stream (no host sync inside the timed loop); read by fmrx_kernel_timing
     std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
@@ -1028,6 +1029,27 @@ int fmrx_synth_device(fmrx_ctx* c, uint64_t seed, int rf_fs, uint64_t first_pair
     return launch_synth(p, c->d_sintab.p, first_pair, n_pairs, d_out, c->stream)
                ? fail(FMRX_EHIP, "synth launch failed")
                : 0;
+}
+
+int fmrx_synth_device_streams(fmrx_ctx* c, const uint64_t* seeds, size_t n_seeds, int rf_fs, uint64_t first_pair,
+                              size_t n_pairs, uint8_t* d_out, size_t stride_bytes) {
+    CtxLock lock_(c);
+    if (!c || !d_out || !seeds || rf_fs <= 0 || n_seeds == 0 || n_seeds > 65535 ||
+        (n_seeds > 1 && stride_bytes < 2 * n_pairs) || (stride_bytes & 1))
+        return fail(FMRX_EINVAL, "bad argument");
+    int rc = set_device(c);
+    if (rc) return rc;
+    std::vector<SynthParams> ps(n_seeds);
+    for (size_t k = 0; k < n_seeds; k++) synth_setup(seeds[k], rf_fs, &ps[k]);
+    if ((rc = c->d_synth_params.ensure(sizeof(SynthParams) * n_seeds))) return rc;
+    // ps is pageable host memory: the stream is drained before it goes out of scope
+    HIPCHK(hipMemcpyAsync(c->d_synth_params.p, ps.data(), sizeof(SynthParams) * n_seeds, hipMemcpyHostToDevice,
+                          c->stream));
+    if (launch_synth_streams(reinterpret_cast<const SynthParams*>(c->d_synth_params.p), (int)n_seeds,
+                             c->d_sintab.p, first_pair, n_pairs, d_out, stride_bytes, c->stream))
+        return fail(FMRX_EHIP, "synth launch failed");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return FMRX_OK;
 }
 
 }  // extern "C"

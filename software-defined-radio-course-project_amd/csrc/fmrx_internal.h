@@ -179,5 +179,8 @@ int launch_normalize(const uint8_t* iq, size_t n_pairs, float* i, float* q, hipS
 int launch_quantize(const float* x, size_t n, int16_t* out, hipStream_t s);
 int launch_synth(const SynthParams& p, const int16_t* d_sintab, uint64_t first, size_t n,
                  uint8_t* out, hipStream_t s);
+// n_streams streams in one launch: stream k (params d_params[k]) at out + k * stride
+int launch_synth_streams(const SynthParams* d_params, int n_streams, const int16_t* d_sintab,
+                         uint64_t first, size_t n, uint8_t* out, size_t stride, hipStream_t s);
 
 }  // namespace fmrx

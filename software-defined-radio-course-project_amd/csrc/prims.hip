@@ -170,6 +170,23 @@ __global__ void synth_kernel(SynthParams p, const int16_t* __restrict__ tab, uin
     }
 }
 
+// One launch for a (stream, sample) grid: blockIdx.y = stream, its parameters from d_params
+// (the generator is position-addressable, so every workgroup fills its own slice).
+__global__ void synth_streams_kernel(const SynthParams* __restrict__ ps, const int16_t* __restrict__ tab,
+                                     uint64_t first, size_t n, uint8_t* __restrict__ out, size_t stride) {
+    __shared__ int16_t lt[kSinSize];
+    for (int i = threadIdx.x; i < kSinSize; i += blockDim.x) lt[i] = tab[i];
+    const SynthParams p = ps[blockIdx.y];
+    uint16_t* o = reinterpret_cast<uint16_t*>(out + (size_t)blockIdx.y * stride);
+    __syncthreads();
+    for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+         k += (size_t)gridDim.x * blockDim.x) {
+        uint8_t iq[2];
+        synth_pair(p, lt, first + k, iq);
+        o[k] = (uint16_t)iq[0] | ((uint16_t)iq[1] << 8);
+    }
+}
+
 inline int ok() { return hipGetLastError() == hipSuccess ? 0 : -2; }
 
 }  // namespace
@@ -250,6 +267,17 @@ int launch_synth(const SynthParams& p, const int16_t* d_sintab, uint64_t first, 
     int blocks = blocks_for(n, 256);
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(synth_kernel, dim3(blocks), dim3(256), 0, s, p, d_sintab, first, n, out);
+    return ok();
+}
+
+int launch_synth_streams(const SynthParams* d_params, int n_streams, const int16_t* d_sintab,
+                         uint64_t first, size_t n, uint8_t* out, size_t stride, hipStream_t s) {
+    if (n == 0 || n_streams <= 0) return 0;
+    int bx = blocks_for(n, 256);
+    const int cap = std::max(1, 8192 / n_streams);  // ~8k workgroups in all: every CU busy, LDS table loads amortised
+    if (bx > cap) bx = cap;
+    hipLaunchKernelGGL(synth_streams_kernel, dim3(bx, n_streams), dim3(256), 0, s, d_params, d_sintab, first, n,
+                       out, stride);
     return ok();
 }
 

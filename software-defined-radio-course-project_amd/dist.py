@@ -75,8 +75,7 @@ def fmrx_process_fn(fmrx, mode: int, channels: int, n_blocks: int, device: int, 
                 return out
             iq = torch.empty((n, n_blocks * bb), dtype=torch.uint8, device=f"cuda:{device}")
             torch.cuda.synchronize(device)
-            for k, sid in enumerate(ids):
-                rx.synth_device(sid, 0, n_blocks * bb // 2, iq[k].data_ptr())
+            rx.synth_device_streams(list(ids), 0, n_blocks * bb // 2, iq.data_ptr(), n_blocks * bb)
             rx.process_device(iq.data_ptr(), n_blocks, out.data_ptr())
             rx.synchronize()
             return out
@@ -84,6 +83,78 @@ def fmrx_process_fn(fmrx, mode: int, channels: int, n_blocks: int, device: int, 
             rx.close()
 
     return process
+
+
+def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, device: int,
+                mode: int = 0, expect: dict | None = None, warmup: bool = True,
+                collective: bool | None = None) -> dict | None:
+    """BASELINE configs[4] as one timed step: `n_streams` independent stereo streams (stream id
+    = synth seed) of `seconds` each, this rank's contiguous shard processed as ONE multi-stream
+    device-resident call, then the S16 PCM gathered to rank 0 (RCCL over xGMI; gloo rehearses
+    it).  Timing = barrier -> process -> gather, max over ranks.  The input is synthesized on the
+    device in one launch before the timed region; `warmup` runs one untimed full-size call first
+    (code objects, scratch sized) and restarts from the power-on state.  `expect` maps stream id
+    -> the reference build's PCM SHA-256 (tests/golden/hashes.json streams_*); rank 0 checks
+    those streams of the gathered PCM.  `collective` (default: world > 1) routes the barrier,
+    gather and timing reduction through the initialised process group; without it (one rank, no
+    process group) the rank's PCM is the result.  Returns rank 0's result dict (None elsewhere)."""
+    import hashlib
+    import time
+
+    ids = list(shard(n_streams, world, rank))
+    rx = fmrx.Receiver(mode, fmrx.STEREO, n_streams=max(1, len(ids)), device=device)
+    try:
+        bb = rx.geo.block_bytes
+        nb = int(seconds * rx.geo.rf_fs * 2 // bb)
+        pcm_len = nb * rx.geo.pcm_samples
+        dev = torch.device("cuda", device)
+        iq = torch.empty((max(1, len(ids)), nb * bb), dtype=torch.uint8, device=dev)
+        out = torch.empty((len(ids), pcm_len), dtype=torch.int16, device=dev)
+        torch.cuda.synchronize(dev)
+        t_synth = time.perf_counter()
+        if ids:
+            rx.synth_device_streams(ids, 0, nb * bb // 2, iq.data_ptr(), nb * bb)
+        t_synth = time.perf_counter() - t_synth
+        if ids and warmup:
+            rx.process_device(iq.data_ptr(), nb, out.data_ptr())
+            rx.synchronize()
+            rx.reset()
+        pg = world > 1 if collective is None else collective
+        if pg:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        if ids:
+            rx.process_device(iq.data_ptr(), nb, out.data_ptr())
+            rx.synchronize()
+        t1 = time.perf_counter()
+        gathered = gather_pcm(out, n_streams, pcm_len, world, rank) if pg else out
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        t = torch.tensor([t2 - t0, t1 - t0, t2 - t1],
+                         device=dev if pg and dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
+        if pg:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        total, proc, gat = (float(v) for v in t)
+        if rank != 0:
+            return None
+        assert gathered.shape == (n_streams, pcm_len), gathered.shape
+        sig_s = nb * bb / 2 / rx.geo.rf_fs
+        res = {"workload": f"BASELINE configs[4]: {n_streams} independent mode-{mode} stereo streams x {sig_s:g} s, "
+                           f"{world} rank(s), streams sharded contiguously"
+                           + (", S16 PCM gathered to rank 0" if pg else ", PCM left on the one rank (no gather)"),
+               "n_gpus": world, "seconds": round(total, 4), "seconds_process": round(proc, 4),
+               "seconds_gather": round(gat, 4), "gather_bytes": int(gathered.numel() * 2),
+               "MS_per_s": round(n_streams * nb * bb / 2 / total / 1e6, 1),
+               "stream_seconds_per_s": round(n_streams * sig_s / total, 1),
+               "x_realtime_per_stream": round(sig_s / total, 2), "synth_seconds_untimed": round(t_synth, 3)}
+        if expect:
+            got = {sid: hashlib.sha256(gathered[sid].cpu().numpy().tobytes()).hexdigest() for sid in expect}
+            res["checked_streams"] = sorted(expect)
+            res["bit_exact_vs_reference"] = all(got[sid] == expect[sid] for sid in expect)
+        return res
+    finally:
+        rx.close()
 
 
 def run_time_sharded(process: Callable[[range], torch.Tensor], n_blocks: int, pcm_per_block: int,

@@ -82,6 +82,7 @@ PROTOTYPES = {
     "fmrx_quantize": (C.c_int, [_vp, _vp, _sz, _vp]),
     "fmrx_synth_host": (C.c_int, [C.c_uint64, C.c_int, C.c_uint64, _sz, _vp]),
     "fmrx_synth_device": (C.c_int, [_vp, C.c_uint64, C.c_int, C.c_uint64, _sz, _vp]),
+    "fmrx_synth_device_streams": (C.c_int, [_vp, _vp, _sz, C.c_int, C.c_uint64, _sz, _vp, _sz]),
     "fmrx_test_pll_fallback": (C.c_int, [_vp, C.c_int, _vp, _vp, _sz, _vp]),
     "fmrx_debug_mono_stamps": (C.c_int, [_vp, _vp, _sz, C.POINTER(_sz)]),
     "fmrx_debug_pll_stats": (C.c_int, [_vp, _vp]),
@@ -279,6 +280,12 @@ class Receiver:
 
     def synth_device(self, seed: int, first_pair: int, n_pairs: int, d_out: int) -> None:
         _check(lib().fmrx_synth_device(self.h, seed, self.geo.rf_fs, first_pair, n_pairs, d_out))
+
+    def synth_device_streams(self, seeds, first_pair: int, n_pairs: int, d_out: int, stride: int) -> None:
+        """One launch for several streams: stream k (seed seeds[k]) at d_out + k * stride bytes."""
+        sd = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64))
+        _check(lib().fmrx_synth_device_streams(self.h, sd.ctypes.data, sd.size, self.geo.rf_fs, first_pair,
+                                               n_pairs, d_out, stride))
 
     def kernel_timing(self, reset: int = 0) -> tuple[float, int]:
         ms, n = C.c_double(), C.c_long()

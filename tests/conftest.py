@@ -89,7 +89,12 @@ def _hashes():
 
 def long_runs():
     """Long-run hashes (2-100 s of signal): pcm, pcm_mono and the last PLL state."""
-    return {k: v for k, v in _hashes().items() if not k.startswith("bench_")}
+    return {k: v for k, v in _hashes().items() if not k.startswith(("bench_", "streams_"))}
+
+
+def stream_runs():
+    """Per-stream PCM hashes of chosen streams of BASELINE configs[4]-shaped runs."""
+    return {k: v for k, v in _hashes().items() if k.startswith("streams_")}
 
 
 def bench_runs():

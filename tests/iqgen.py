@@ -35,6 +35,20 @@ def load_fmrx():
     return load_module("fmrx")
 
 
+def stream_hashes(n_streams: int, n_blocks: int) -> dict:
+    """stream id -> the reference build's PCM SHA-256 for mode-0 stereo streams of n_blocks
+    blocks (stream id = synth seed), from tests/golden/hashes.json streams_* (BASELINE
+    configs[4]-shaped runs); empty when none is recorded for that length."""
+    import json
+
+    with open(os.path.join(REPO, "tests", "golden", "hashes.json")) as f:
+        h = json.load(f)
+    for k, v in h.items():
+        if k.startswith("streams_") and v["n_blocks"] == n_blocks:
+            return {int(s): d for s, d in v["pcm_sha256"].items() if int(s) < n_streams}
+    return {}
+
+
 def splitmix64(x: np.ndarray) -> np.ndarray:
     x = x.astype(np.uint64)
     with np.errstate(over="ignore"):

@@ -24,7 +24,7 @@ def _run(*extra):
 
 
 def test_bench_json_contract():
-    j = _run("--no-cpu-baseline")
+    j = _run("--no-cpu-baseline", "--streams-seconds", "0.5")
     for k, t in (("metric", str), ("value", float), ("unit", str), ("n_gpus", int), ("steps", int),
                  ("warmup", int), ("ms_per_step", float), ("higher_is_better", bool), ("scaling", str),
                  ("dtype", str), ("data", str), ("config", dict), ("roofline", dict)):
@@ -40,6 +40,11 @@ def test_bench_json_contract():
     for c in ("configs[2]", "configs[3]"):
         assert oc[c]["input_matches_fixture"] is True, oc[c]
         assert oc[c]["bit_exact_vs_reference"] is True, oc[c]
+    # configs[4] (256 stereo streams; 0.5 s each here, 60 s by default) checked against the
+    # reference build's per-stream hashes
+    c4 = oc["configs[4]"]
+    assert "error" not in c4, c4
+    assert c4["n_gpus"] == 1 and c4["checked_streams"] == [0, 7, 8, 15] and c4["bit_exact_vs_reference"] is True
     rf = j["roofline"]
     assert rf["bound"] in ("hbm", "mfma") and rf["unit"] in ("GB/s", "TFLOP/s")
     assert 0 < rf["frac"] < 1 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3

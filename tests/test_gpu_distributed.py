@@ -82,5 +82,8 @@ def test_configs4_rccl_one_rank_bench_streams(fmrx):
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     line = [l for l in r.stdout.decode().splitlines() if l.startswith("{")][-1]
     res = json.loads(line)
-    assert res["n_gpus"] == 1 and "RCCL" in res["config"]
+    assert res["n_gpus"] == 1 and res["backend"] == "RCCL"
     assert res["gather_bytes"] == 16 * int(0.5 * 2400000 * 2 // 12800) * 256 * 2
+    # the gathered PCM against the reference build's hashes (tests/golden/hashes.json
+    # streams_c4_short), not against another GPU run
+    assert res["checked_streams"] == [0, 7, 8, 15] and res["bit_exact_vs_reference"] is True

@@ -708,6 +708,15 @@ def test_device_synth_equals_host(fmrx):
         rx.synth_device(9, 123456, 300001, d.data_ptr())
         rx.synchronize()
         assert np.array_equal(d.cpu().numpy(), fmrx.synth_host(9, 2400000, 123456, 300001))
+        # several streams in one launch (configs[4]'s per-rank input), rows with a gap between
+        seeds, n, stride = [5, 300, 7, 2**40 + 3], 70001, 2 * 70001 + 6
+        m = torch.full((len(seeds) * stride,), 0xAB, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        rx.synth_device_streams(seeds, 999, n, m.data_ptr(), stride)
+        rows = m.cpu().numpy()
+        for k, sd in enumerate(seeds):
+            assert np.array_equal(rows[k * stride:k * stride + 2 * n], fmrx.synth_host(sd, 2400000, 999, n)), sd
+            assert (rows[k * stride + 2 * n:(k + 1) * stride] == 0xAB).all()  # nothing past the row
 
 
 # ---- the PLL's fallback libm (refused arguments) against glibc ---------------------------------
