@@ -431,7 +431,7 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
                                                            size_t stride, const double* side, size_t seg, double step,
                                                            float norm_bw, const float* st, float* out_base,
                                                            size_t ostride, int* fail, float2* rec, size_t rb,
-                                                           int inject, int sat_ok) {
+                                                           int inject, int sat_ok, int pred_ok) {
     const int t = threadIdx.x & 63;
     const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int s_lane = wave * spw + ((t >> 4) & (spw - 1));
@@ -448,6 +448,7 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
     const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
     PllState p{S[0], S[1], S[2], S[3], S[5]};
     if (sat_ok && pll_sat_segment(spw, p.trig, step)) return;  // pll_sat_kernel's (pll_sat.hip)
+    if (pred_ok && pll_pred_wave(p.trig, step)) return;        // pll_pred_kernel's (pll_pred.hip)
     const int nb = n / NB;
     if (owner) fail[s] = nb;
     PllCtx ctx{};
@@ -918,9 +919,14 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         return e ? std::atoi(e) : -1;
     }();
     const bool spec = spec_env && (reinterpret_cast<uintptr_t>(io) & 15) == 0 && stride % 4 == 0;
-    // FMRX_PLL_SAT=0 (measurements, tests): saturated segments on the ordinary runner too
+    // FMRX_PLL_SAT=0 / FMRX_PLL_PRED=0 (measurements, tests): saturated segments / segments from
+    // 2^20 steps on the ordinary runner too
     const int sat_ok = [] {
         const char* e = std::getenv("FMRX_PLL_SAT");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    const int pred_ok = [] {
+        const char* e = std::getenv("FMRX_PLL_PRED");
         return (e && e[0] == '0') ? 0 : 1;
     }();
     int spw = 1;
@@ -947,11 +953,15 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         if (spec) {
             if (spw <= 4) {
                 hipLaunchKernelGGL(pll_spec_lane_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw, stride,
-                                   side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject, sat_ok);
+                                   side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject, sat_ok, pred_ok);
                 // saturated streams (pll_sat_segment), which the lane kernel leaves to it
                 if (sat_ok && spw == 1)
                     launch_pll_sat(grid, block, s, x, m, n_streams, spw, stride, side, seg, step, norm_bw, st, args,
                                    seg, fail, rec, rb, inject);
+                // waves from trigOffset 2^20 below the stick (pll_pred_wave)
+                if (pred_ok)
+                    launch_pll_pred(grid, block, s, x, m, n_streams, spw, stride, side, seg, step, norm_bw, st, args,
+                                    seg, fail, rec, rb, inject);
             } else
                 hipLaunchKernelGGL(pll_spec_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw,
                                    stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);

@@ -679,6 +679,69 @@ def test_pll_saturated_runner(fmrx, orc, monkeypatch, inject, sat, freq, nco_sca
         assert (resumed > 0) if inject is not None else (resumed == 0), (resumed, checked)
 
 
+@pytest.mark.parametrize("trig0", [1048576.0, 4194321.0, 16772216.0, 1048575.0])
+@pytest.mark.parametrize("inject", [None, "5"])
+@pytest.mark.parametrize("pred", ["1", "0"])
+def test_pll_predicted_runner(fmrx, orc, monkeypatch, trig0, inject, pred):
+    """Segments from trigOffset 2^20 up to the 2^24 stick: the predicted-trigArg runner
+    (pll_pred.hip; FMRX_PLL_PRED=0: the lane runner), starting at 2^20, at 2^22 + 17, and 5,000
+    steps below the stick (its pr stops rising inside the segment); 2^20 - 1 stays on the lane
+    runner.  A corrupted batch must be caught and resumed; without it every batch verifies."""
+    monkeypatch.setenv("FMRX_PLL_PRED", pred)
+    if inject is not None:
+        monkeypatch.setenv("FMRX_PLL_SPEC_INJECT", inject)
+    n = 20000
+    rng = np.random.default_rng(int(trig0) % 1000)
+    t = np.arange(n)
+    x = (0.1 * np.cos(2 * np.pi * 19000 / 240000 * t + 0.7) + 0.02 * rng.standard_normal(n)).astype(np.float32)
+    st0 = np.array([-3e-4, -0.9, 0.6, 0.8, 1.0, trig0], np.float32)
+    want_x, want_st = orc.pll(x, 19000, 240000, 2.0, 0.0, 0.01, st0)
+    with fmrx.Receiver(0, fmrx.STEREO) as rx:
+        buf = _d(x)
+        st = _d(st0)
+        counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+        rx.debug_pll_stats(counts.data_ptr())
+        torch.cuda.synchronize()
+        rx.pll(buf.data_ptr(), n, 19000, 240000, 2.0, 0.0, 0.01, st.data_ptr())
+        rx.synchronize()
+        rx.debug_pll_stats(None)
+        assert same(buf.cpu().numpy(), want_x)
+        assert same(st.cpu().numpy(), want_st)
+        resumed, checked = counts.cpu().tolist()
+        assert checked == n // 16
+        assert (resumed > 0) if inject is not None else (resumed == 0), (resumed, checked)
+
+
+def test_predicted_runner_rows(fmrx):
+    """pll_pred.hip with two streams a wave (1,100 streams: 16-lane rows), every stream put at
+    its own trigOffset in [2^21, 2^21 + 1100) through the state blob -- except stream 5, at
+    1,000, which sends its wave (streams 4 and 5) to the lane runner -- 40 blocks in one call,
+    every batch verified, and streams on both sides compared with the same stream alone."""
+    ns, nb, bb = 1100, 40, 12800
+    ins = np.stack([iqgen.make("synth:%d" % (700 + s % 5), (nb + 2) * bb) for s in range(ns)])
+    with fmrx.Receiver(0, fmrx.STEREO, n_streams=ns) as rx:
+        rx.process(ins[:, : 2 * bb])
+        blob = bytearray(rx.get_state())
+        hdr = np.frombuffer(bytes(blob[:40]), np.uint32)
+        pll_off = 40 + ns * (int(hdr[6]) + 4 * int(hdr[7]) + 4 * 64)
+        pll = np.frombuffer(bytes(blob[pll_off: pll_off + ns * 32]), np.float32).reshape(ns, 8).copy()
+        pll[:, 5] = 2097152.0 + np.arange(ns, dtype=np.float32)
+        pll[5, 5] = 1000.0
+        blob[pll_off: pll_off + ns * 32] = pll.tobytes()
+        rx.set_state(bytes(blob))
+        counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+        rx.debug_pll_stats(counts.data_ptr())
+        out = rx.process(ins[:, 2 * bb:])
+        rx.debug_pll_stats(None)
+    resumed, checked = counts.cpu().tolist()
+    assert checked > 0 and resumed == 0, (resumed, checked)
+    for s in (0, 4, 5, 6, 1023, 1099):
+        with fmrx.Receiver(0, fmrx.STEREO) as r1:
+            r1.process(ins[s, : 2 * bb])
+            r1.set_state(_stream_blob(bytes(blob), r1.get_state(), ns, s))
+            assert np.array_equal(r1.process(ins[s, 2 * bb:]), out[s]), s
+
+
 def test_quantize_and_elementwise(fmrx, orc):
     x = np.array([0, 1, -1, 1.99993896484375, 2, -2, 2.5, 1e6, -1e6, 1.4e5, np.inf, -np.inf, np.nan,
                   131071.99, -131072, 3.05e-5] * 4, np.float32)
