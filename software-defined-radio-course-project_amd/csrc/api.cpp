@@ -120,6 +120,26 @@ struct fmrx_ctx {
     bool timing = false;
     unsigned long long* stamps = nullptr;  // fmrx_debug_mono_stamps (diagnostic)
     unsigned long long* pll_stats = nullptr;  // fmrx_debug_pll_stats (diagnostic)
+    int n_simd = 1024;                        // SIMDs of cfg.device (4 per CU), set at creation
+    // bounds on the streams' trigOffset (PllHint) of the stereo and the RDS PLL: 0 after a reset,
+    // advanced by every call's samples (the float increments stick at 2^24), re-read from the
+    // blob by fmrx_set_state; unknown after a failed launch
+    struct TrigTrack {
+        bool known = true;
+        double lo = 0.0, hi = 0.0;
+        void advance(size_t n) {
+            lo = std::min(lo + (double)n, 16777216.0);
+            hi = std::min(hi + (double)n, 16777216.0);
+        }
+    } pll_trig, rds_trig;
+    PllHint hint(const TrigTrack& t) const {
+        PllHint h;
+        h.n_simd = n_simd;
+        h.known = t.known;
+        h.trig_lo = t.lo;
+        h.trig_hi = t.hi;
+        return h;
+    }
 };
 
 namespace {
@@ -155,6 +175,8 @@ int set_device(const fmrx_ctx* c) {
 
 int reset_state(fmrx_ctx* c) {
     const int ns = c->cfg.n_streams;
+    c->pll_trig = fmrx_ctx::TrigTrack{};
+    c->rds_trig = fmrx_ctx::TrigTrack{};
     HIPCHK(hipMemsetAsync(c->d_halo[0].p, 0x80, c->halo_bytes * ns, c->stream));
     HIPCHK(hipMemsetAsync(c->d_halo[1].p, 0x80, c->halo_bytes * ns, c->stream));
     c->halo_cur = 0;
@@ -222,7 +244,12 @@ int run_rds(fmrx_ctx* c, const float* d_demod, size_t demod_stride, size_t n_if,
     L.ca = c->d_rds_taps.p + kRdsTaps;
     L.bp_fs = (float)c->geo.bp_fs;
     L.n_if = (int)n_if;
-    if (launch_rds(L, ns, c->stream)) return fail(FMRX_EHIP, "RDS launch failed");
+    L.hint = c->hint(c->rds_trig);
+    if (launch_rds(L, ns, c->stream)) {
+        c->rds_trig.known = false;
+        return fail(FMRX_EHIP, "RDS launch failed");
+    }
+    c->rds_trig.advance(n_if);
     if (d_nco)
         HIPCHK(hipMemcpyAsync(d_nco, c->d_rds_car.p, sizeof(float) * n_if * ns, hipMemcpyDeviceToDevice,
                               c->stream));
@@ -250,11 +277,7 @@ int mono_segments(const fmrx_ctx* c, long long n_if) {
 // overrides it (0 = equal segments; timing sweeps).
 constexpr int kOlderShare = 620;
 int mono_older_share(const fmrx_ctx* c, int segs) {
-    static const int n_simd = [] {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        return 4 * cus;
-    }();
+    const int n_simd = c->n_simd;
     int share = kOlderShare;
     if (const char* e = std::getenv("FMRX_MONO_SPLIT")) share = std::atoi(e);
     if (share <= 0 || share >= 1024) return 0;
@@ -375,8 +398,11 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
     // project.cpp:166: PLL(carrier, 19000, if_fs, 2, 0, 0.01, ...)
     if ((rc = c->d_pll_side.ensure(pll_side_doubles((int)n_if, ns)))) return rc;
     if (launch_pll(c->d_carrier.p, (int)n_if, ns, n_if, 19000.0f, (float)c->geo.if_fs, 2.0f, 0.0f,
-                   0.01f, c->d_pll.p, c->d_pll_side.p, c->stream, c->pll_stats))
+                   0.01f, c->d_pll.p, c->d_pll_side.p, c->stream, c->hint(c->pll_trig), c->pll_stats)) {
+        c->pll_trig.known = false;
         return fail(FMRX_EHIP, "PLL launch failed");
+    }
+    c->pll_trig.advance(n_if);
     AudioLaunch A{};
     A.demod = c->d_demod.p;
     A.demod_stride = c->demod_stride;
@@ -509,6 +535,11 @@ int fmrx_create(const fmrx_config* cfg, fmrx_ctx** out) {
                     g.rf_decim);
     }
     if ((rc = set_device(c))) { delete c; return rc; }
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess && cus > 0)
+            c->n_simd = 4 * cus;
+    }
     // taps, exactly as the reference designs them (project.cpp:37, 97, 104, 117)
     c->rf.resize(g.rf_taps);
     design_lpf(c->rf.data(), (float)g.rf_fs, (float)kRfFc, g.rf_taps, 1);
@@ -651,11 +682,17 @@ int state_io(fmrx_ctx* c, uint8_t* buf, size_t bytes, bool put) {
                                     (uint32_t)c->geo.rf_taps, (uint32_t)c->cfg.n_streams, (uint32_t)c->halo_bytes,
                                     (uint32_t)c->audio_hist, c->audio_hist_stale ? 1u : 0u, 0u};
     if (put) {
-        if (std::memcmp(hdr, buf, 8 * sizeof(uint32_t)) != 0)
-            return fail(FMRX_ESTATE, "state blob does not match this context");
-        uint32_t flags;
-        std::memcpy(&flags, buf + 8 * sizeof(uint32_t), sizeof flags);
-        if (flags > 1u) return fail(FMRX_ESTATE, "state blob: unknown flags 0x%x", flags);
+        uint32_t got[kStateHdrWords];
+        std::memcpy(got, buf, sizeof got);
+        if (got[0] != kStateMagic) return fail(FMRX_ESTATE, "not an fmrx state blob (magic 0x%08x)", got[0]);
+        if (got[1] != kStateVersion)
+            return fail(FMRX_ESTATE, "state blob version %u, expected %u (INTEGRATION.md: blob versions)", got[1],
+                        kStateVersion);
+        if (std::memcmp(hdr + 2, got + 2, 6 * sizeof(uint32_t)) != 0)
+            return fail(FMRX_ESTATE, "state blob is for another context shape (mode %u, channels %u, rf_taps %u, "
+                        "%u streams)", got[2], got[3], got[4], got[5]);
+        if (got[8] > 1u) return fail(FMRX_ESTATE, "state blob: unknown flags 0x%x", got[8]);
+        if (got[9] != 0u) return fail(FMRX_ESTATE, "state blob: reserved word 9 is 0x%x, must be 0", got[9]);
     } else {
         std::memcpy(buf, hdr, sizeof hdr);
     }
@@ -695,6 +732,22 @@ int fmrx_set_state(fmrx_ctx* c, const void* buf, size_t bytes) {
         uint32_t flags;
         std::memcpy(&flags, p + 8 * sizeof(uint32_t), sizeof flags);
         c->audio_hist_stale = (flags & 1u) != 0;
+        // the streams' trigOffsets (state_io order: halo, audio history, demod history, PLL x 8)
+        const size_t ns = c->cfg.n_streams;
+        const uint8_t* pll = p + kStateHdrWords * sizeof(uint32_t) +
+                             ns * (c->halo_bytes + sizeof(float) * (c->audio_hist + kDemodHist));
+        fmrx_ctx::TrigTrack t;
+        t.lo = 16777216.0;
+        t.hi = 0.0;
+        for (size_t s = 0; s < ns; s++) {
+            float v;
+            std::memcpy(&v, pll + (8 * s + 5) * sizeof(float), sizeof v);
+            if (!(v >= 0.0f && v <= 16777216.0f && v == std::floor(v))) t.known = false;
+            t.lo = std::min(t.lo, (double)v);
+            t.hi = std::max(t.hi, (double)v);
+        }
+        if (!t.known) t.lo = t.hi = 0.0;
+        c->pll_trig = t;
     }
     return rc;
 }
@@ -960,8 +1013,10 @@ int fmrx_pll(fmrx_ctx* c, float* d_io, int n, float freq, float fs, float nco_sc
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(c->d_scratch.p, d_st, 6 * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
     if ((rc = c->d_pll_side.ensure(pll_side_doubles(n, 1)))) return rc;
+    PllHint hint;  // the state is the caller's: trigOffset unknown
+    hint.n_simd = c->n_simd;
     if (launch_pll(d_io, n, 1, (size_t)n, freq, fs, nco_scale, phase_adjust, norm_bw, c->d_scratch.p,
-                   c->d_pll_side.p, c->stream, c->pll_stats))
+                   c->d_pll_side.p, c->stream, hint, c->pll_stats))
         return fail(FMRX_EHIP, "launch failed");
     HIPCHK(hipMemcpyAsync(d_st, c->d_scratch.p, 6 * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
     return FMRX_OK;

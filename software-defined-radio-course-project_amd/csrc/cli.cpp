@@ -114,7 +114,7 @@ int main(int argc, char** argv) {
         mode = std::atoi(pos[0]);
         channels = std::atoi(pos[1]);
         if (mode < 0 || mode > 3) { std::fprintf(stderr, "Invalid mode: %d!\n", mode); return 1; }
-        if (channels < 1 || channels > 2) { std::fprintf(stderr, "Invalid channel: %d!\n", channels); return 1; }
+        if (channels < 1 || channels > 2) { std::fprintf(stderr, "Invaild channel: %d!\n", channels); return 1; }  // project.cpp:289, verbatim
     } else {  // :292-298
         usage(argv[0]);
         return 1;

@@ -92,9 +92,19 @@ int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s);
 // not verify to spec_stats[0] and the batches checked to spec_stats[1].
 constexpr size_t kPllSeg = (size_t)1 << 18;  // at most this many samples per stream per PLL segment
 size_t pll_side_doubles(int n, int n_streams);
+// What the host knows when it launches a PLL (api.cpp tracks it per context): the device's SIMD
+// count (streams per wave) and, when `known`, bounds on every stream's trigOffset at the call's
+// start (integer-valued, <= 2^24: the reference's float increments from a reset), so that
+// launch_pll enqueues only the runners some segment can use.  Unknown (the fmrx_pll primitive's
+// state lives in caller memory): every runner is launched and each takes its own waves.
+struct PllHint {
+    int n_simd = 1024;
+    bool known = false;
+    double trig_lo = 0.0, trig_hi = 0.0;
+};
 int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
                float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s,
-               unsigned long long* spec_stats = nullptr);
+               const PllHint& hint, unsigned long long* spec_stats = nullptr);
 
 // pll_sat.hip: the saturated-segment runner over a launch_pll segment (pll_spec_lane_kernel's grid
 // and arguments; it runs the streams that one leaves to it)
@@ -148,6 +158,7 @@ struct RdsLaunch {
     const float* ca;        // 113.5-114.5 kHz taps (device)
     float bp_fs;
     int n_if;
+    PllHint hint;           // the RDS PLL's (launch_pll)
 };
 int launch_rds(const RdsLaunch& L, int n_streams, hipStream_t s);
 

@@ -107,7 +107,7 @@ int launch_rds(const RdsLaunch& L, int n_streams, hipStream_t s) {
     hipLaunchKernelGGL(rds_front_kernel, dim3((L.n_if + kTile - 1) / kTile, n_streams), dim3(kTile), 0, s, L);
     // project.cpp:259: PLL(carrier_data, 114000, bp_fs, 0.5, 0, 0.01, ...), in place -> NCO
     if (launch_pll(L.carrier, L.n_if, n_streams, L.car_stride, 114000.0f, L.bp_fs, 0.5f, 0.0f, 0.01f,
-                   L.pll, L.pll_side, s))
+                   L.pll, L.pll_side, s, L.hint))
         return -2;
     hipLaunchKernelGGL(rds_mix_kernel, dim3((L.n_if + 255) / 256, n_streams), dim3(256), 0, s, L);
     hipLaunchKernelGGL(rds_state_kernel, dim3(n_streams), dim3(128), 0, s, L);

@@ -895,7 +895,7 @@ size_t pll_side_doubles(int n, int n_streams) {
 // 16-byte aligned; the plain path is pll_kernel in place.
 int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
                float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s,
-               unsigned long long* spec_stats) {
+               const PllHint& hint, unsigned long long* spec_stats) {
     if (n <= 0) return 0;
     const size_t seg = pll_seg_len(n, n_streams);
     const size_t rb = seg / kPllBatch;
@@ -903,11 +903,7 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     float2* rec = reinterpret_cast<float2*>(args + seg * (size_t)n_streams);      // rb per stream
     int* fail = reinterpret_cast<int*>(rec + rb * (size_t)n_streams);
     // one stream per wave while the waves fit one per SIMD, then more streams per wave
-    static const int n_simd = [] {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        return 4 * cus;
-    }();
+    const int n_simd = hint.n_simd;
     const bool spec_env = [] {  // read per call: tests switch it within one process
         const char* e = std::getenv("FMRX_PLL_SPEC");
         return !(e && e[0] == '0');
@@ -939,7 +935,18 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
 
     // filter.cpp:163: 2*PI*(freq/Fs) in double from the float quotient (host == device IEEE)
     const double step = (2.0 * 3.14159265358979323846) * static_cast<double>(freq / fs);  // dy4.h:14 PI
+    const bool step_ok = std::fabs(step * (double)kPllTrigStick) < kPllMaxPr;
     for (size_t off = 0; off < (size_t)n; off += seg) {
+        // the runners a segment can need (pll_sat_segment / pll_pred_wave take their waves, the
+        // lane kernel the rest): with known trigOffset bounds the others are not launched
+        const double lo = std::min(hint.trig_lo + (double)off, (double)kPllTrigStick);
+        const double hi = std::min(hint.trig_hi + (double)off, (double)kPllTrigStick);
+        const bool k = hint.known && step_ok;
+        const bool all_sat = k && sat_ok && spw == 1 && lo >= (double)kPllTrigStick;
+        const bool all_pred = k && pred_ok && lo >= (double)kPllPredMin && hi < (double)kPllTrigStick;
+        const bool run_lane = !(all_sat || all_pred);
+        const bool run_sat = sat_ok && spw == 1 && (!k || hi >= (double)kPllTrigStick);
+        const bool run_pred = pred_ok && (!k || (hi >= (double)kPllPredMin && lo < (double)kPllTrigStick));
         const int m = (int)std::min(seg, (size_t)n - off);
         float* x = io + off;
         if (spw <= 4)  // the split kernels read stream-major side data
@@ -952,14 +959,16 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         const size_t ostride = spec ? seg : stride;
         if (spec) {
             if (spw <= 4) {
-                hipLaunchKernelGGL(pll_spec_lane_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw, stride,
-                                   side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject, sat_ok, pred_ok);
+                if (run_lane)
+                    hipLaunchKernelGGL(pll_spec_lane_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw,
+                                       stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject,
+                                       run_sat ? 1 : 0, run_pred ? 1 : 0);  // it leaves waves only to those launched
                 // saturated streams (pll_sat_segment), which the lane kernel leaves to it
-                if (sat_ok && spw == 1)
+                if (run_sat)
                     launch_pll_sat(grid, block, s, x, m, n_streams, spw, stride, side, seg, step, norm_bw, st, args,
                                    seg, fail, rec, rb, inject);
                 // waves from trigOffset 2^20 below the stick (pll_pred_wave)
-                if (pred_ok)
+                if (run_pred)
                     launch_pll_pred(grid, block, s, x, m, n_streams, spw, stride, side, seg, step, norm_bw, st, args,
                                     seg, fail, rec, rb, inject);
             } else

@@ -167,6 +167,59 @@ def test_state_blob_keeps_seek_staleness(fmrx):
             rx2.audio_block(demod)
 
 
+def test_state_blob_header_errors(fmrx):
+    """fmrx_set_state names what is wrong with a foreign blob: another format version, another
+    context shape, a non-zero reserved word (FMRX_ESTATE each, the context unchanged)."""
+    with fmrx.Receiver(0, fmrx.STEREO) as rx, fmrx.Receiver(0, fmrx.MONO) as other:
+        good = rx.get_state()
+        for word, val, msg in ((1, 1, "version 1, expected 2"), (0, 7, "not an fmrx state blob"),
+                               (9, 5, "reserved word 9")):
+            bad = bytearray(good)
+            bad[4 * word: 4 * word + 4] = np.uint32(val).tobytes()
+            with pytest.raises(fmrx.FmrxError) as e:
+                rx.set_state(bytes(bad))
+            assert e.value.code == fmrx.FMRX_ESTATE and msg in str(e.value), str(e.value)
+        with pytest.raises(fmrx.FmrxError) as e:
+            rx.set_state(other.get_state() + bytes(len(good)))
+        assert "another context shape" in str(e.value)
+        rx.set_state(good)
+
+
+def test_trig_hint_after_set_state(fmrx, monkeypatch):
+    """The host-side trigOffset bounds that pick which PLL runners launch (api.cpp TrigTrack)
+    follow a restored blob: a stream restored at 2^20 - 2,000 crosses into the predicted
+    runner's range within the call and one at 2^24 - 3,000 into the saturated runner's; the PCM
+    equals the lane runner's alone (FMRX_PLL_PRED=0, FMRX_PLL_SAT=0: every segment on it), and
+    every batch verified -- a runner left out by a wrong bound would leave its waves unrun."""
+    bb = oracle.MODES[0][0]
+    iq = iqgen.make("synth:91", 30 * bb)
+
+    def run(trig):
+        with fmrx.Receiver(0, fmrx.STEREO) as rx:
+            blob = bytearray(rx.get_state())
+            hdr = np.frombuffer(bytes(blob[:40]), np.uint32)
+            pll_off = 40 + int(hdr[6]) + 4 * int(hdr[7]) + 4 * 64
+            pll = np.frombuffer(bytes(blob[pll_off: pll_off + 32]), np.float32).copy()
+            pll[5] = trig
+            blob[pll_off: pll_off + 32] = pll.tobytes()
+            rx.set_state(bytes(blob))
+            counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+            rx.debug_pll_stats(counts.data_ptr())
+            got = rx.process(iq)
+            rx.debug_pll_stats(None)
+        return got, counts.cpu().tolist()
+
+    for trig in (1048576.0 - 2000, 16777216.0 - 3000):
+        got, (resumed, checked) = run(trig)
+        assert checked > 0 and resumed == 0, (trig, resumed, checked)
+        monkeypatch.setenv("FMRX_PLL_PRED", "0")
+        monkeypatch.setenv("FMRX_PLL_SAT", "0")
+        want, _ = run(trig)
+        monkeypatch.delenv("FMRX_PLL_PRED")
+        monkeypatch.delenv("FMRX_PLL_SAT")
+        assert np.array_equal(got, want), trig
+
+
 @pytest.mark.parametrize("mode,nb", [(2, 6), (3, 4)])
 def test_polyphase_mono_split_resume_and_mixed_api(fmrx, orc, mode, nb):
     """Modes 2/3 run the rational resampler inside the fused kernel; its history must survive

@@ -106,7 +106,8 @@ def test_cli_built_and_usage(fmrx):
     exe = os.path.join(REPO, "software-defined-radio-course-project_amd", "bin", "fmrx")
     assert os.access(exe, os.X_OK)
     for args, msg in ((["7", "1"], b"Invalid mode"), (["-1", "2"], b"Invalid mode"),
-                      (["0", "3"], b"Invalid channel"), (["0", "1", "2"], b"Usage"),
+                      (["0", "3"], b"Invaild channel"),  # project.cpp:289 spells it so
+                      (["0", "1", "2"], b"Usage"),
                       (["--bogus"], b"Usage")):
         r = subprocess.run([exe] + args, capture_output=True, timeout=60)
         assert r.returncode == 1 and msg in r.stderr, (args, r.stderr)
