@@ -48,7 +48,7 @@ int main(int argc, char** argv) {
     const float nb = 0.01f;
     const float Kp = nb * (float)2.666, Ki = nb * nb * (float)3.555;
     const double w = 2 * 3.14159265358979323846 * (double)(19000.0f / 240000.0f);
-    const size_t N = std::min(x.size(), (size_t)1 << 24);  // unsaturated steps: trigOffset < 2^24
+    const size_t N = x.size();  // steps from 2^24 on: trigOffset stuck (pll_sat.hip's regime)
     std::vector<float> phase(N), arg(N);
     float integ = 0, ph = 0, fbI = 1, fbQ = 0, trig = 0;
     for (size_t i = 0; i < N; i++) {
@@ -64,7 +64,7 @@ int main(int argc, char** argv) {
         fbQ = (float)std::sin((double)a);
     }
     // ranges of j (step index = trigOffset - 1)
-    const size_t edges[] = {0, 1u << 16, 1u << 20, 1u << 22, 1u << 23, 1u << 24};
+    const size_t edges[] = {0, 1u << 16, 1u << 20, 1u << 22, 1u << 23, 1u << 24, N};
     const int batches[] = {1, 4, 8, 16};
     // lookback: the candidate's phase is the one at the end of batch b - lb (lb = 1: the
     // previous batch; lb = 2 lets the candidates of batch b + 1 be evaluated during batch b)
@@ -78,7 +78,7 @@ int main(int argc, char** argv) {
     std::printf("phase range [%g, %g]\n", pmin, pmax);
     std::printf("%-22s %5s %9s %9s %9s %9s %12s\n", "j range", "B", "k=0", "|k|<=1", "|k|<=2", "|k|>2",
                 "batch|k|<=1");
-    for (int r = 0; r + 1 < 6; r++) {
+    for (int r = 0; r + 1 < 7; r++) {
         const size_t j0 = edges[r], j1 = std::min(edges[r + 1], N);
         if (j0 >= j1) continue;
         for (int B : batches) {
@@ -89,7 +89,7 @@ int main(int argc, char** argv) {
                 bool ok = true;
                 for (size_t j = b0; j < b0 + B && j < j1; j++) {
                     if (j < j0) continue;
-                    const float cand = (float)(w * (double)(float)(j + 1) + (double)p0);
+                    const float cand = (float)(w * (double)std::min((float)(j + 1), 16777216.0f) + (double)p0);
                     const long k = std::labs(ulps_between(cand, arg[j]));
                     if (k == 0) k0++;
                     if (k <= 1) k1++;
@@ -104,6 +104,33 @@ int main(int argc, char** argv) {
             std::printf("[2^%-4.1f, 2^%-4.1f)     %5d %9.4f %9.4f %9.4f %9.4f %12.4f\n", j0 ? std::log2((double)j0) : 0.0,
                         std::log2((double)j1), B, k0 / tot, k1 / tot, k2 / tot, kx / tot,
                         (double)nb_ok / nb_all);
+        }
+    }
+    // two candidates: c0 and its neighbour on the side of the exact sum P + phase_ref (the
+    // rounding's direction), batches of B with lookback lb
+    std::printf("two candidates (c0 and the neighbour towards P + phase_ref):\n");
+    for (int r = 2; r + 1 < 7; r++) {
+        const size_t j0 = edges[r], j1 = std::min(edges[r + 1], N);
+        if (j0 >= j1) continue;
+        for (int B : {8, 16}) {
+            long hit = 0, nb_all = 0, nb_ok = 0;
+            for (size_t b0 = (j0 / B) * B; b0 < j1; b0 += B) {
+                const size_t back = (size_t)(lb - 1) * B + 1;
+                const float p0 = b0 >= back ? phase[b0 - back] : 0.0f;
+                bool ok = true;
+                for (size_t j = b0; j < b0 + B && j < j1; j++) {
+                    const double sum = w * (double)std::min((float)(j + 1), 16777216.0f) + (double)p0;
+                    const float c0 = (float)sum;
+                    const float c1 = std::nextafter(c0, sum > (double)c0 ? INFINITY : -INFINITY);
+                    const bool h = arg[j] == c0 || arg[j] == c1;
+                    hit += h;
+                    ok = ok && h;
+                }
+                nb_all++;
+                nb_ok += ok;
+            }
+            std::printf("[2^%-4.1f, 2^%-4.1f)     %5d  step hit %.4f  batch hit %.4f\n", std::log2((double)j0),
+                        std::log2((double)j1), B, (double)hit / (double)(j1 - j0), (double)nb_ok / nb_all);
         }
     }
     return 0;
