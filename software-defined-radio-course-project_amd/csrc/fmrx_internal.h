@@ -112,11 +112,12 @@ void launch_pll_sat(dim3 grid, dim3 block, hipStream_t s, const float* io, int n
                     size_t stride, const double* side, size_t seg, double step, float norm_bw, const float* st,
                     float* out, size_t ostride, int* fail, float2* rec, size_t rb, int inject);
 
-// pll_pred.hip: the predicted-trigArg runner (segments from trigOffset 2^20 below the 2^24 stick),
-// same grid and arguments; it runs the waves pll_spec_lane_kernel leaves to it (pll_pred_wave)
-void launch_pll_pred(dim3 grid, dim3 block, hipStream_t s, const float* io, int n, int n_streams, int spw,
-                     size_t stride, const double* side, size_t seg, double step, float norm_bw, const float* st,
-                     float* out, size_t ostride, int* fail, float2* rec, size_t rb, int inject);
+// pll_pred.hip: the predicted-trigArg runner (segments from trigOffset 2^20, the stick included),
+// pll_spec_lane_kernel's arguments, one two-wave workgroup per group of spw streams; it runs the
+// groups that kernel leaves to it (pll_pred_wave)
+void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_streams, int spw, size_t stride,
+                     const double* side, size_t seg, double step, float norm_bw, const float* st, float* out,
+                     size_t ostride, int* fail, float2* rec, size_t rb, int inject, int sat_ok);
 
 // test hook: the PLL's fallback libm on device (kind 0 sincos, 1 atan2, 2 NCO cos)
 int launch_pll_fallback_test(int kind, const float* a, const float* b, size_t n, float* out, hipStream_t s);

@@ -93,13 +93,14 @@ __device__ inline bool pll_sat_segment(int spw, float trig0, double step) {
     return spw == 1 && trig0 == kPllTrigStick && fabs(step * (double)kPllTrigStick) < kPllMaxPr;
 }
 
-// A stream for pll_pred_kernel: trigOffset in [2^20, 2^24) at the segment start (integer-valued,
+// A stream for pll_pred_kernel: trigOffset in [2^20, 2^24] at the segment start (integer-valued,
 // as pll_side needs), where the predicted trigArgs almost always hit (pll_pred.hip).  The wave
 // takes the predicted runner only if every stream of it qualifies (ballot: all lanes alike), and
-// pll_spec_lane_kernel makes the same test to leave exactly those waves to it.
+// pll_spec_lane_kernel makes the same test to leave exactly those waves to it; saturated waves go
+// to pll_sat_kernel first when it is launched.
 constexpr float kPllPredMin = 1048576.0f;  // 2^20
 __device__ inline bool pll_pred_wave(float trig0, double step) {
-    const bool ok = trig0 >= kPllPredMin && trig0 < kPllTrigStick && trig0 == floorf(trig0) &&
+    const bool ok = trig0 >= kPllPredMin && trig0 <= kPllTrigStick && trig0 == floorf(trig0) &&
                     fabs(step * (double)kPllTrigStick) < kPllMaxPr;
     return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }

@@ -942,11 +942,10 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         const double lo = std::min(hint.trig_lo + (double)off, (double)kPllTrigStick);
         const double hi = std::min(hint.trig_hi + (double)off, (double)kPllTrigStick);
         const bool k = hint.known && step_ok;
-        const bool all_sat = k && sat_ok && spw == 1 && lo >= (double)kPllTrigStick;
-        const bool all_pred = k && pred_ok && lo >= (double)kPllPredMin && hi < (double)kPllTrigStick;
-        const bool run_lane = !(all_sat || all_pred);
+        const bool sat_all = k && sat_ok && spw == 1 && lo >= (double)kPllTrigStick;  // every wave saturated
+        const bool run_lane = !(k && lo >= (double)kPllPredMin && (pred_ok || sat_all));
         const bool run_sat = sat_ok && spw == 1 && (!k || hi >= (double)kPllTrigStick);
-        const bool run_pred = pred_ok && (!k || (hi >= (double)kPllPredMin && lo < (double)kPllTrigStick));
+        const bool run_pred = pred_ok && (!k || hi >= (double)kPllPredMin) && !sat_all;
         const int m = (int)std::min(seg, (size_t)n - off);
         float* x = io + off;
         if (spw <= 4)  // the split kernels read stream-major side data
@@ -969,8 +968,8 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
                                    seg, fail, rec, rb, inject);
                 // waves from trigOffset 2^20 below the stick (pll_pred_wave)
                 if (run_pred)
-                    launch_pll_pred(grid, block, s, x, m, n_streams, spw, stride, side, seg, step, norm_bw, st, args,
-                                    seg, fail, rec, rb, inject);
+                    launch_pll_pred(waves, s, x, m, n_streams, spw, stride, side, seg, step, norm_bw, st, args, seg,
+                                    fail, rec, rb, inject, run_sat ? 1 : 0);
             } else
                 hipLaunchKernelGGL(pll_spec_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw,
                                    stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);

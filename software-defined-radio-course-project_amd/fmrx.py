@@ -15,7 +15,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "libfmrx.so")
+# FMRX_LIB_PATH: an A/B build of the same sources (Makefile `ab` target; measurements only)
+LIB_PATH = os.environ.get("FMRX_LIB_PATH") or os.path.join(PKG_DIR, "libfmrx.so")
 HEADER = os.path.join(REPO, "include", "fmrx.h")
 
 FMRX_OK, FMRX_EINVAL, FMRX_EHIP, FMRX_ENOMEM, FMRX_ESTATE = 0, -1, -2, -3, -4
