@@ -47,6 +47,7 @@ namespace fmrx {
 // A/B build only (Makefile `ab`, AB=-DFMRX_AB_PROF): shader-clock cycles of the two waves, body vs
 // barrier wait, summed over every batch and workgroup, printed at exit
 __device__ unsigned long long g_pred_prof[6];
+__device__ unsigned long long g_pipe_prof[6];
 #define PROF_T() __builtin_amdgcn_s_memtime()
 #else
 #define PROF_T() 0ull
@@ -71,26 +72,46 @@ __device__ inline float pred_e(float a, float v, double iv) {
     return (float)fma(Y, iv, B);
 }
 
-// The smallest double S with float(S) >= c, for a positive float c given by its bits cb: the
-// midpoint of c and its predecessor (exact in double), or the double just above it when the
-// tie rounds down (ties to even: an odd c loses it).  trigArg = float(S) with S = P + phase in
-// double, so float(S) >= c is S >= thr_of(c): the chain selects a candidate by comparing the
-// double sum it forms anyway, without waiting for its rounding to float.
-__device__ inline double thr_of(uint32_t cb) {
-    const double m = 0.5 * ((double)__builtin_bit_cast(float, cb - 1u) + (double)__builtin_bit_cast(float, cb));
-    return (cb & 1u) ? __builtin_bit_cast(double, __builtin_bit_cast(uint64_t, m) + 1ull) : m;
+// Adjacent floats, across zero too (the phase may sit near it).
+__device__ inline float f_up(float x) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, x);
+    return __builtin_bit_cast(float, (u & 0x80000000u) ? (u == 0x80000000u ? 1u : u - 1u) : u + 1u);
+}
+__device__ inline float f_down(float x) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, x);
+    return __builtin_bit_cast(float, (u & 0x80000000u) ? u + 1u : (u == 0u ? 0x80000001u : u - 1u));
+}
+
+// trigArg = float(P + phase) in double (filter.cpp:165) is monotone in the float phase, so
+// "trigArg >= c" is "phase >= T" for a float threshold T: the smallest phase whose trigArg
+// reaches c.  The chain then selects its candidate with float compares of the phase it has just
+// formed, before the double sum and its roundings.  T lies within an ulp of float(m - P), m the
+// boundary of c's rounding interval (the midpoint with its predecessor, the tie rounding to
+// even): the first of its two lower neighbours, itself and its upper neighbour that reaches c,
+// checked by the double sum itself, exactly; -inf flags a T outside that window (the caller
+// poisons the step's candidates, so the chain takes it as a miss).
+__device__ inline bool reaches(double P, float ph, float c) { return (float)(P + (double)ph) >= c; }
+__device__ inline float phase_thr(double P, uint32_t cb) {
+    const float c = __builtin_bit_cast(float, cb);
+    const double m = 0.5 * ((double)__builtin_bit_cast(float, cb - 1u) + (double)c);
+    const float f0 = (float)(m - P), fm = f_down(f0), fmm = f_down(fm), fp = f_up(f0);
+    const bool rp = reaches(P, fp, c), r0 = reaches(P, f0, c), rm = reaches(P, fm, c), rmm = reaches(P, fmm, c);
+    const float T = rm ? fm : (r0 ? f0 : fp);
+    return (rp && !rmm) ? T : -__builtin_inff();
 }
 
 template <int NB>
 __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, int n_streams, int spw, size_t stride,
                                                       const double* side, size_t seg, double step, float norm_bw,
                                                       const float* st, float* out_base, size_t ostride, int* fail,
-                                                      float2* rec, size_t rb, int inject, int sat_ok) {
-    // per step of the batch, double-buffered by batch parity: (e_m, e_0, e_p, bits of c0 - 1 ulp),
-    // the thresholds (thr_of(c0), thr_of(c0 + 1 ulp)) and P
-    __shared__ float4 cand[2][4][NB];
-    __shared__ double2 thr[2][4][NB];
-    __shared__ double prs_l[2][4][NB];
+                                                      float2* rec, size_t rb, int inject, int sat_ok,
+                                                      int pipe_on) {
+    // per step of the batch, double-buffered by batch parity: the phase thresholds of c0 and
+    // c0 + 1 ulp, the bits of c0 - 1 ulp and the next step's e for c0 - 1 ulp (sa); its e for c0
+    // and c0 + 1 ulp and P (sb: e_0, e_p, P as two words).  Two 16-B reads a step: the chain
+    // loads a whole batch into registers before its first step.
+    __shared__ float4 sa[2][4][NB];
+    __shared__ float4 sb[2][4][NB];
     __shared__ float ph[2][4];  // the phase at the start of batch k, slot k & 1
     const int t = threadIdx.x & 63;
     const bool chain = threadIdx.x < 64;
@@ -106,7 +127,9 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
     const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
     PllState p{S[0], S[1], S[2], S[3], S[5]};
     // both waves alike: the lane runner's waves, or the saturated runner's when it is launched
-    if (!pll_pred_wave(p.trig, step) || (sat_ok && pll_sat_segment(spw, p.trig, step))) return;
+    if (!pll_pred_wave(p.trig, step) || (sat_ok && pll_sat_segment(spw, p.trig, step)) ||
+        (pipe_on && pll_pipe_stream(p.trig, step)))
+        return;
     const int nb = n / NB;
     if (nb < 2) {  // batch 0 alone, exactly (no barrier is reached)
         if (chain) {
@@ -137,29 +160,38 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
         auto put = [&](int b, float phase_ref, float v, double iv, double pr) {
             const float c0 = (float)(pr + (double)phase_ref);
             const uint32_t cb = __builtin_bit_cast(uint32_t, c0);
-            // a candidate that is not a positive finite float: every trigArg misses it
-            const uint32_t cmb = (c0 > 0.0f && c0 < 3.0e38f) ? cb - 1u : 0xFFFFFFFFu;
+            const uint2 prw = __builtin_bit_cast(uint2, pr);
             if (spw == 1) {
                 // one stream: its four rows share the work -- rows 0-2 the e of candidates
-                // c0 - 1, c0, c0 + 1 ulp, row 3 the miss bits, thresholds and P
+                // c0 - 1, c0, c0 + 1 ulp, row 3 the thresholds, the miss bits and P
                 const int r = t >> 4;
-                float* slot = reinterpret_cast<float*>(&cand[b & 1][0][l]);
+                float* a = reinterpret_cast<float*>(&sa[b & 1][0][l]);
+                float* bb = reinterpret_cast<float*>(&sb[b & 1][0][l]);
                 if (r < 3) {
-                    slot[r] = pred_e(__builtin_bit_cast(float, cb + (uint32_t)(r - 1)), v, iv);
+                    const float e = pred_e(__builtin_bit_cast(float, cb + (uint32_t)(r - 1)), v, iv);
+                    if (r == 0) a[3] = e;
+                    else bb[r - 1] = e;
                 } else {
-                    slot[3] = __builtin_bit_cast(float, cmb);
-                    thr[b & 1][0][l] = make_double2(thr_of(cb), thr_of(cb + 1u));
-                    prs_l[b & 1][0][l] = pr;
+                    const float T0 = phase_thr(pr, cb), T1 = phase_thr(pr, cb + 1u);
+                    // a candidate that is not a positive finite float or a threshold outside its
+                    // window: every trigArg misses the step's candidates
+                    const bool ok = c0 > 0.0f && c0 < 3.0e38f && T0 > -__builtin_inff() && T1 > -__builtin_inff();
+                    a[0] = T0;
+                    a[1] = T1;
+                    a[2] = __builtin_bit_cast(float, ok ? cb - 1u : 0xFFFFFFFFu);
+                    bb[2] = __builtin_bit_cast(float, prw.x);
+                    bb[3] = __builtin_bit_cast(float, prw.y);
                 }
                 return;
             }
             const float em = pred_e(__builtin_bit_cast(float, cb - 1u), v, iv);
             const float e0 = pred_e(c0, v, iv);
             const float ep = pred_e(__builtin_bit_cast(float, cb + 1u), v, iv);
+            const float T0 = phase_thr(pr, cb), T1 = phase_thr(pr, cb + 1u);
+            const bool ok = c0 > 0.0f && c0 < 3.0e38f && T0 > -__builtin_inff() && T1 > -__builtin_inff();
             if ((t >> 4) < spw) {
-                cand[b & 1][q][l] = make_float4(em, e0, ep, __builtin_bit_cast(float, cmb));
-                thr[b & 1][q][l] = make_double2(thr_of(cb), thr_of(cb + 1u));
-                prs_l[b & 1][q][l] = pr;
+                sa[b & 1][q][l] = make_float4(T0, T1, __builtin_bit_cast(float, ok ? cb - 1u : 0xFFFFFFFFu), em);
+                sb[b & 1][q][l] = make_float4(e0, ep, __builtin_bit_cast(float, prw.x), __builtin_bit_cast(float, prw.y));
             }
         };
         // ring of 4 batches of step data: batch k in slot k & 3, refilled right after its use,
@@ -221,16 +253,14 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
         if (owner) rec[(size_t)s * rb] = make_float2(p.integ, p.phase);
     }
     float integ = p.integ, phase = p.phase;
-    // Sd: the double sum P + phase of the last step done (trigArg = float(Sd)); batch 0's last
-    // trigArg comes from the exact path, where only its float is known -- the carry's three
-    // slots are alike, so the selection does not depend on Sd there
-    double Sd = ctx.x;
-    float4 carry_a;
-    double2 carry_d;
+    float tlast = (float)ctx.x;  // the last trigArg done
+    // the carry: the candidates of the previous batch's last trigArg -- after the exact batch 0
+    // its e directly (all three slots alike, so the thresholds do not matter)
+    float4 carry_a, carry_b;
     {
-        const float e = pred_e((float)ctx.x, x[NB], ivs[NB]);
-        carry_a = make_float4(e, e, e, __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, (float)ctx.x) - 1u));
-        carry_d = make_double2(0.0, 0.0);
+        const float e = pred_e(tlast, x[NB], ivs[NB]);
+        carry_a = make_float4(0.0f, 0.0f, __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, tlast) - 1u), e);
+        carry_b = make_float4(e, e, 0.0f, 0.0f);
     }
     if (l == 0) ph[1][q] = phase;  // the start of batch 1, for the evaluator's batch 2
     __syncthreads();               // (prologue)
@@ -238,68 +268,80 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
     for (int b = 1; b < nb; b++) {
         const unsigned long long p0 = PROF_T();
         const int bp = b & 1;
-        const float integ0 = integ, phase0 = phase;
-        const double Sd0 = Sd;
-        // step J: the e of candidate float(S_{J-1}) among those of trigArg_{J-1} (batch b - 1's
-        // last step for J = 0: the carry), chosen by comparing S_{J-1} with their thresholds
-        auto cand_of = [&](auto jc, float4& a, double2& d) {
+        const float integ0 = integ, phase0 = phase, tlast0 = tlast;
+        // the whole batch's data into registers first (32 reads), so no step waits on LDS
+        float4 A[NB], Bv[NB];
+#pragma unroll
+        for (int J = 0; J < NB; J++) {
+            A[J] = sa[bp][q][J];
+            Bv[J] = sb[bp][q][J];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        auto P_of = [&](int J) {
+            return __builtin_bit_cast(double, make_uint2(__builtin_bit_cast(uint32_t, Bv[J].z),
+                                                         __builtin_bit_cast(uint32_t, Bv[J].w)));
+        };
+        // step J's selection data: those of trigArg_{J-1} (the carry for J = 0)
+        auto sel_of = [&](auto jc, float4& a, float4& bb) {
             constexpr int J = decltype(jc)::value;
             if constexpr (J == 0) {
                 a = carry_a;
-                d = carry_d;
+                bb = carry_b;
             } else {
-                a = cand[bp][q][J - 1];
-                d = thr[bp][q][J - 1];
+                a = A[J - 1];
+                bb = Bv[J - 1];
             }
         };
         float o[NB];
         // max over the steps of bits(trigArg) - bits(c0 - 1 ulp): > 2 is a miss.  It starts with
         // the previous batch's last trigArg against the carry: a miss there (also left by that
         // batch's redo, which does not reach the step after it) is this batch's step 0
-        uint32_t dmax = __builtin_bit_cast(uint32_t, (float)Sd0) - __builtin_bit_cast(uint32_t, carry_a.w);
+        uint32_t dmax = __builtin_bit_cast(uint32_t, tlast) - __builtin_bit_cast(uint32_t, carry_a.z);
         unroll_ic(
             [&](auto jc) {
                 constexpr int J = decltype(jc)::value;
-                float4 a;
-                double2 d;
-                cand_of(jc, a, d);
-                const float e = Sd >= d.y ? a.z : (Sd >= d.x ? a.y : a.x);
+                float4 a, bb;
+                sel_of(jc, a, bb);
+                // the chain: two compares of the phase, e, (Ki e, Kp e), the three float updates
+                const float e = phase >= a.y ? bb.y : (phase >= a.x ? bb.x : a.w);
                 const float2v k = float2v{Ki, Kp} * e;
                 integ = integ + k.x;
                 phase = phase + (k.y + integ);
-                Sd = prs_l[bp][q][J] + (double)phase;
-                const float arg = (float)Sd;
+                // off the chain: trigArg (filter.cpp:165) and its candidate check
+                const float arg = (float)(P_of(J) + (double)phase);
                 o[J] = arg;
-                dmax = max(dmax, __builtin_bit_cast(uint32_t, arg) - __builtin_bit_cast(uint32_t, cand[bp][q][J].w));
+                dmax = max(dmax, __builtin_bit_cast(uint32_t, arg) - __builtin_bit_cast(uint32_t, A[J].z));
             },
             std::make_integer_sequence<int, NB>{});
+        tlast = o[NB - 1];
         if (__builtin_expect(dmax > 2u, 0)) {
             // a trigArg outside its candidates: redo the batch, evaluating the e of a step that
             // follows a miss directly (rows without a miss are masked off here)
             integ = integ0;
             phase = phase0;
-            Sd = Sd0;
+            float tprev = tlast0;
             const int j0 = b * NB;
             unroll_ic(
                 [&](auto jc) {
                     constexpr int J = decltype(jc)::value;
-                    float4 a;
-                    double2 d;
-                    cand_of(jc, a, d);
-                    float e = Sd >= d.y ? a.z : (Sd >= d.x ? a.y : a.x);
-                    const float ta = (float)Sd;
-                    if (__builtin_bit_cast(uint32_t, ta) - __builtin_bit_cast(uint32_t, a.w) > 2u)
-                        e = pred_e(ta, x[j0 + J], ivs[j0 + J]);
+                    float4 a, bb;
+                    sel_of(jc, a, bb);
+                    float e = phase >= a.y ? bb.y : (phase >= a.x ? bb.x : a.w);
+                    if (__builtin_bit_cast(uint32_t, tprev) - __builtin_bit_cast(uint32_t, a.z) > 2u)
+                        e = pred_e(tprev, x[j0 + J], ivs[j0 + J]);
                     const float2v k = float2v{Ki, Kp} * e;
                     integ = integ + k.x;
                     phase = phase + (k.y + integ);
-                    Sd = prs_l[bp][q][J] + (double)phase;
-                    o[J] = (float)Sd;
+                    tprev = (float)(P_of(J) + (double)phase);
+                    o[J] = tprev;
                 },
                 std::make_integer_sequence<int, NB>{});
+            tlast = o[NB - 1];
         }
-        phase += (inject >= 0 && b == 1 + (inject + s) % (nb - 1)) ? 1.0e-3f : 0.0f;  // test hook
-        if (inject >= 0) Sd = prs_l[bp][q][NB - 1] + (double)phase;
+        if (inject >= 0 && b == 1 + (inject + s) % (nb - 1)) {  // test hook: a wrong batch
+            phase += 1.0e-3f;
+            tlast = (float)(P_of(NB - 1) + (double)phase);
+        }
         // every lane stores: the rows of a stream hold the same values, and rows past the last
         // stream recompute it bit for bit (their evaluator rows too), so the writes agree
         float* ob = out + b * NB;
@@ -307,8 +349,8 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
         for (int qq = 0; qq < NB / 4; qq++)
             reinterpret_cast<float4*>(ob)[qq] = *reinterpret_cast<const float4*>(&o[4 * qq]);
         rec[(size_t)s * rb + b] = make_float2(integ, phase);
-        carry_a = cand[bp][q][NB - 1];  // the candidates of step 15: step 0 of batch b + 1
-        carry_d = thr[bp][q][NB - 1];
+        carry_a = A[NB - 1];  // the candidates of step 15: step 0 of batch b + 1
+        carry_b = Bv[NB - 1];
         if (l == 0) ph[(b + 1) & 1][q] = phase;
         const unsigned long long p1 = PROF_T();
         __syncthreads();
@@ -326,27 +368,399 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
     (void)ch_wait;
 }
 
+
+// ---- pll_pipe_kernel: one stream a workgroup of three waves, trigOffset from 2^22 on ----------
+//
+// pll_pred_kernel's chain wave issues ~16 VALU a step (the candidate choice, the updates, trigArg
+// and its check) and one wave issues a VALU per ~4 cycles, dependent or not
+// (tools/ubench_dep.hip, profiles/r03/ubench_dep.txt): its step costs its instruction count.  Here
+// the chain keeps only the recurrence -- the choice by two sign masks and bitfield inserts (no
+// VCC and its wait states), (Ki e, Kp e), the three float updates: ten VALU a step -- and hands
+// its phases to the other waves:
+//   wave 1: batch b + 2's e for the three candidates (lane (r, l): candidate c0 - 1 + r of step l);
+//   wave 2: rows 0-1 the phase thresholds of c0 and c0 + 1 ulp, c0's bits and P of batch b + 2;
+//           row 2 batch b - 1's trigArgs float(P + phase) (filter.cpp:165), their check against the
+//           candidates and the output stores.
+// Batch b + 2's candidates come from the phase at the start of batch b (tools/pll_predict.cpp
+// lookback 3), so the chain reads batch b + 1's data -- 20 16-byte reads at once -- right after
+// batch b's steps, where the reads overlap its phase stores and the barrier (spread over the
+// steps they stall it more: tools/ubench_chain.hip, profiles/r03/ubench_chain.txt).  A batch
+// whose trigArg missed its candidates -- E2 flags it in the interval after the chain ran it, the
+// chain reads the flag at the end of the next one -- is redone on the exact path with the two
+// after it (pll_redo from the recorded state); every wave takes two more barriers around that
+// redo, and the evaluators then redo batches b + 1 and b + 2 from the corrected phases.  From 2^22 the three
+// candidates held on every step of the bench stream (tools/pll_predict.cpp), so this is rare; the
+// output goes through pll_check_kernel like every runner's.
+
+// The chain's candidate choice, e of trigArg_{j-1} from the phase: a = (T0, T1, e(c0 - 1),
+// e(c0)), ep = e(c0 + 1); phase < T0 -> c0 - 1, < T1 -> c0, else c0 + 1, by the sign bits of
+// the exact differences (arithmetic shifts to masks, bitfield inserts).  One asm block: as
+// separate statements the compiler pads each with a wait state, and left to itself it turns
+// the select into compare + v_cndmask (a VCC write and its wait states).
+__device__ inline float pick(float phase, float4 a, float ep) {
+    float e;
+    uint32_t d0, d1;
+    asm("v_sub_f32 %1, %3, %4\n"
+        "v_sub_f32 %2, %3, %5\n"
+        "v_ashrrev_i32 %1, 31, %1\n"
+        "v_ashrrev_i32 %2, 31, %2\n"
+        "v_bfi_b32 %1, %1, %6, %7\n"
+        "v_bfi_b32 %0, %2, %1, %8"
+        : "=&v"(e), "=&v"(d0), "=&v"(d1)
+        : "v"(phase), "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(ep));
+    return e;
+}
+
+// NB-step batches (pll_check_kernel's), BPI of them an interval of NI = NB BPI steps: one
+// barrier an interval; RD intervals of step data in flight in the evaluators' load ring.
+// One wave a SIMD (amdgpu_waves_per_eu): the register budget is the chain's, so the scheduler
+// keeps each burst of reads whole instead of threading it through the steps for occupancy.
+template <int NB, int BPI, int RD>
+__global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))) pll_pipe_kernel(const float* io, int n, int n_streams, size_t stride,
+                                                      const double* side, size_t seg, double step, float norm_bw,
+                                                      const float* st, float* out_base, size_t ostride, int* fail,
+                                                      float2* rec, size_t rb, int inject) {
+    constexpr int NI = NB * BPI;
+    static_assert(NI == 32 || NI == 64, "the evaluators' lane map: 64 / NI lanes a step");
+    constexpr int LPS = 64 / NI;  // evaluator lanes a step
+    constexpr int CH = 32;        // the chain's steps a burst of reads
+    // rings of four intervals (interval k in slot k & 3; interval 0 is batch 0): per step the
+    // thresholds T0, T1 and the e of c0 - 1 ulp and c0 (sel), the e of c0 + 1 ulp (sep),
+    // bits(c0) - 1 (scb), P (spr); the chain's phases (sph); per interval the check's verdict
+    // (smiss) and "redone exactly" (sexact)
+    __shared__ float4 sel[4][NI];
+    __shared__ float sep[4][NI];
+    __shared__ uint32_t scb[4][NI];
+    __shared__ double spr[4][NI];
+    __shared__ float sph[4][NI];
+    __shared__ int smiss[4], sexact[4];
+    const int w = threadIdx.x >> 6, t = threadIdx.x & 63, l = t & (NI - 1), h = t / NI;
+    const int s = blockIdx.x;  // grid = n_streams
+    const float* x = io + (size_t)s * stride;
+    float* out = out_base + (size_t)s * ostride;
+    const float* S = st + 8 * (size_t)s;
+    const float Kp = norm_bw * static_cast<float>(2.666);
+    const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
+    PllState p{S[0], S[1], S[2], S[3], S[5]};
+    if (!pll_pipe_stream(p.trig, step)) return;  // uniform over the group
+    const float trig0 = p.trig;
+    const int nb = n / NB;
+    const int ni = (nb - 1) / BPI;  // intervals after batch 0
+    const int inj = inject >= 0 && nb > 1 ? 1 + (inject + s) % (nb - 1) : -1;  // test hook: a wrong batch
+    // batches [k0, k1) exactly from state p (ctx): outputs, records, the test hook
+    auto exact = [&](PllState& q, PllCtx& c, int k0, int k1) {
+        for (int k = k0; k < k1; k++) {
+            const PllPair z = pll_redo(q, c, x + k * NB, out + k * NB, NB, Ki, Kp, step, true);
+            q = z.p;
+            c = z.ctx;
+            if (k == inj) q.phase += 1.0e-3f;
+            if (t == 0) rec[(size_t)s * rb + k] = make_float2(q.integ, q.phase);
+        }
+    };
+    if (ni < 2) {  // a short segment: every batch exactly (no barrier is reached)
+        if (w == 0) {
+            if (t == 0) fail[s] = nb;
+            PllCtx c{};
+            c.valid = false;
+            exact(p, c, 0, nb);
+        }
+        return;
+    }
+    const double* ivs = side + (size_t)s * seg;
+    const double* prs = side + seg * (size_t)n_streams + (size_t)s * seg;
+    auto j0 = [](int k) { return NB + (k - 1) * NI; };  // interval k's first step (k >= 1)
+
+    if (w > 0) {
+        // ring of RD intervals of step data, interval k in slot k % RD, loaded RD - 1 ahead
+        float vq[RD];
+        double ivq[RD], prq[RD];
+        auto ld = [&](int k, float& v, double& iv, double& pr) {
+            const int j = j0(k <= ni ? k : ni) + l;
+            const int jn = min(j + 1, n - 1);  // the step the e is for
+            v = x[jn];
+            iv = ivs[jn];
+            pr = prs[j];
+        };
+        // interval k's candidate data from phase_ref, the phase at the start of interval k - 1:
+        // E1 lane (h, l) the e of candidates c0 - 1 + r of step l, r = h, h + LPS, ... < 3; E2
+        // lane (h, l) the thresholds of c0 + r, r = h, h + LPS, ... < 2, lanes h = 0 also c0's
+        // bits and P
+        auto put = [&](int k, float phase_ref, float v, double iv, double pr) {
+            const float c0 = (float)(pr + (double)phase_ref);
+            const uint32_t cb = __builtin_bit_cast(uint32_t, c0);
+            const int sl = k & 3;
+            if (w == 1) {
+                for (int r = h; r < 3; r += LPS) {
+                    const float e = pred_e(__builtin_bit_cast(float, cb + (uint32_t)(r - 1)), v, iv);
+                    if (r == 0) sel[sl][l].z = e;
+                    else if (r == 1) sel[sl][l].w = e;
+                    else sep[sl][l] = e;
+                }
+            } else {
+                for (int r = h; r < 2; r += LPS) {
+                    const float T = phase_thr(pr, cb + (uint32_t)r);
+                    if (r == 0) sel[sl][l].x = T;
+                    else sel[sl][l].y = T;
+                }
+                if (h == 0) {
+                    scb[sl][l] = cb - 1u;
+                    spr[sl][l] = pr;
+                }
+            }
+        };
+        // E2 lanes h = 0: interval k's trigArgs (filter.cpp:165), stored, and checked against
+        // their candidates: a candidate that is not a positive finite float or a threshold
+        // outside its window (-inf) counts as a miss
+        auto check = [&](int k) {
+            if (w != 2 || h != 0) return;
+            const int sl = k & 3;
+            if (sexact[sl]) {  // redone exactly: the chain stored it
+                if (l == 0) smiss[sl] = 0;
+                return;
+            }
+            const float a = (float)(spr[sl][l] + (double)sph[sl][l]);
+            out[j0(k) + l] = a;
+            const uint32_t cm = scb[sl][l];
+            const float4 tt = sel[sl][l];
+            const float c0 = __builtin_bit_cast(float, cm + 1u);
+            const bool bad = (__builtin_bit_cast(uint32_t, a) - cm > 2u) || !(tt.x > -__builtin_inff()) ||
+                             !(tt.y > -__builtin_inff()) || !(c0 > 0.0f && c0 < 3.0e38f);
+            bool any = __builtin_amdgcn_ballot_w64(bad) != 0;
+#ifdef FMRX_AB_NOREAD
+            any = false;
+#endif
+            if (l == 0) smiss[sl] = any ? 1 : 0;
+        };
+#pragma unroll
+        for (int u = 0; u < RD; u++) ld(1 + u, vq[(1 + u) % RD], ivq[(1 + u) % RD], prq[(1 + u) % RD]);
+        put(1, p.phase, vq[1 % RD], ivq[1 % RD], prq[1 % RD]);  // interval 1 from the initial phase
+        ld(1 + RD, vq[1 % RD], ivq[1 % RD], prq[1 % RD]);
+        __syncthreads();  // (prologue)
+        unsigned long long ev_body = 0, ev_wait = 0;
+        // interval i: interval i + 1's data, interval i - 1's check; groups of RD intervals from
+        // i0 = 1 (mod RD), so the ring slots are compile-time
+        for (int i0 = 1; i0 <= ni; i0 += RD) {
+            unroll_ic(
+                [&](auto uc) {
+                    constexpr int u = decltype(uc)::value;
+                    constexpr int sl = (2 + u) % RD;  // slot of interval i + 1
+                    const int i = i0 + u;
+                    if (i <= ni) {
+                        const unsigned long long p0 = PROF_T();
+                        if (i + 1 <= ni) {
+                            put(i + 1, sph[(i - 1) & 3][NI - 1], vq[sl], ivq[sl], prq[sl]);
+                            ld(i + 1 + RD, vq[sl], ivq[sl], prq[sl]);
+                        }
+                        check(i - 1);
+                        const int redo = __builtin_amdgcn_readfirstlane(smiss[(i - 2) & 3]);
+                        if (redo) {
+                            __syncthreads();  // the chain redoes intervals i - 2 .. i
+                            __syncthreads();
+                            if (i + 1 <= ni) {  // interval i + 1 again, from the corrected phase
+                                float v;
+                                double iv, pr;
+                                ld(i + 1, v, iv, pr);
+                                put(i + 1, sph[(i - 1) & 3][NI - 1], v, iv, pr);
+                            }
+                        }
+                        const unsigned long long p1 = PROF_T();
+                        __syncthreads();
+                        ev_body += p1 - p0;
+                        ev_wait += PROF_T() - p1;
+                    }
+                },
+                std::make_integer_sequence<int, RD>{});
+        }
+        check(ni);
+        __syncthreads();  // the chain reads the last two verdicts
+#ifdef FMRX_AB_PROF
+        if (t == 0 && w == 1) {
+            atomicAdd(&g_pipe_prof[2], ev_body);
+            atomicAdd(&g_pipe_prof[3], ev_wait);
+        }
+#endif
+        (void)ev_body;
+        (void)ev_wait;
+        return;
+    }
+
+    // ---- the chain
+    if (t == 0) fail[s] = nb;
+    PllCtx ctx{};
+    ctx.valid = false;
+    exact(p, ctx, 0, 1);  // batch 0 on the exact path (see pll_spec_kernel)
+    float integ = p.integ, phase = p.phase;
+    // the carry: step 0's candidate data (those of the previous interval's last trigArg); after
+    // an exact stretch that trigArg's e itself in all three slots
+    float4 carry;
+    float carry_ep;
+    auto carry_exact = [&](float a, int k) {
+        const int j = min(j0(k), n - 1);
+        const float e = pred_e(a, x[j], ivs[j]);
+        carry = make_float4(0.0f, 0.0f, e, e);
+        carry_ep = e;
+    };
+    carry_exact((float)ctx.x, 1);
+    if (t == 0) {
+        sph[0][NI - 1] = phase;  // the start of interval 1, for the evaluators' interval 2
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            smiss[k] = 0;
+            sexact[k] = k == 0;
+        }
+    }
+    __syncthreads();  // (prologue)
+    unsigned long long ch_body = 0, ch_wait = 0, n_redo = 0;
+    for (int i = 1; i <= ni; i++) {
+        const unsigned long long p0 = PROF_T();
+        const int is = i & 3;
+        const int flag = smiss[(i - 2) & 3];  // the verdict on interval i - 2 (slot 3 is clear at i = 1)
+        const int kb = 1 + (i - 1) * BPI;         // the interval's first batch
+        // in bursts of CH steps: the data, 1.25 CH 16-byte reads at once in the order the steps
+        // need them (spread over the steps they stall the chain more, tools/ubench_chain.hip),
+        // then the steps, then their phases and batch records
+        float4 A[CH];
+        float EP[CH];
+        unroll_ic(
+            [&](auto hc) {
+                constexpr int H = decltype(hc)::value;
+#ifdef FMRX_AB_NOREAD  // A/B timing only (wrong results): the first burst's data throughout
+                if (i == 1)
+#endif
+#pragma unroll
+                for (int q = 0; q < CH / 4; q++) {
+                    *reinterpret_cast<float4*>(&EP[4 * q]) = reinterpret_cast<const float4*>(&sep[is][H * CH])[q];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) A[4 * q + u] = sel[is][H * CH + 4 * q + u];
+                }
+                float PH[CH];
+                float2 brec[CH / NB];  // (integ, phase) at the end of each batch of the burst
+                unroll_ic(
+                    [&](auto jc) {
+                        constexpr int J = decltype(jc)::value;
+                        const float4 a = J == 0 ? carry : A[J > 0 ? J - 1 : 0];
+                        const float ep = J == 0 ? carry_ep : EP[J > 0 ? J - 1 : 0];
+                        const float e = pick(phase, a, ep);
+                        const float2v k = float2v{Ki, Kp} * e;
+                        integ = integ + k.x;
+                        phase = phase + (k.y + integ);
+                        PH[J] = phase;
+                        if constexpr (J % NB == NB - 1) brec[J / NB] = make_float2(integ, phase);
+                    },
+                    std::make_integer_sequence<int, CH>{});
+                if constexpr (H == NI / CH - 1) {
+                    if (inj >= kb && inj < kb + BPI) {  // test hook, at the interval's end
+                        phase += 1.0e-3f;
+                        brec[CH / NB - 1].y = phase;
+                    }
+                }
+                if (t == 0) {
+#pragma unroll
+                    for (int q = 0; q < CH / 4; q++)
+                        reinterpret_cast<float4*>(&sph[is][H * CH])[q] = *reinterpret_cast<const float4*>(&PH[4 * q]);
+#pragma unroll
+                    for (int q = 0; q < CH / NB; q++) rec[(size_t)s * rb + kb + H * (CH / NB) + q] = brec[q];
+                }
+                carry = A[CH - 1];
+                carry_ep = EP[CH - 1];
+            },
+            std::make_integer_sequence<int, NI / CH>{});
+        if (t == 0) sexact[is] = 0;
+        if (__builtin_amdgcn_readfirstlane(flag)) {
+            n_redo++;
+            __syncthreads();  // E2's stores of interval i - 1 happen before the redo's
+            // intervals i - 2 (missed), i - 1 and i exactly, from the state recorded before
+            const int f = i - 2;
+            const int kf = 1 + (f - 1) * BPI;
+            const float2 r0 = rec[(size_t)s * rb + kf - 1];
+            const float a = (float)(prs[j0(f) - 1] + (double)r0.y);  // the trigArg before it
+            PllState q;
+            PllCtx c{};
+            pll_state_at(q, c, r0.x, r0.y, trig0, (long long)j0(f), a, DeviceLib{});
+            for (int k = f; k <= i; k++) {
+                const int k0 = 1 + (k - 1) * BPI;
+                exact(q, c, k0, k0 + BPI);
+                if (t == 0) {
+                    sph[k & 3][NI - 1] = q.phase;
+                    if (k > f) sexact[k & 3] = 1;
+                }
+            }
+            if (t == 0) smiss[(i - 1) & 3] = 0;  // E2's verdict on the wrong interval i - 1
+            integ = q.integ;
+            phase = q.phase;
+            carry_exact((float)c.x, i + 1);
+            __syncthreads();  // the evaluators redo interval i + 1 from here
+        }
+        const unsigned long long p1 = PROF_T();
+        __syncthreads();
+        ch_body += p1 - p0;
+        ch_wait += PROF_T() - p1;
+    }
+    __syncthreads();  // E2's checks of the last two intervals
+    // a miss in them: from the first missed interval on exactly; then the batches past the last
+    // interval exactly
+    const int f = smiss[(ni - 1) & 3] ? ni - 1 : (smiss[ni & 3] ? ni : ni + 1);
+    const int kf = 1 + (f - 1) * BPI;
+    const float2 r0 = f <= ni ? rec[(size_t)s * rb + kf - 1] : make_float2(integ, phase);
+    if (kf < nb) {
+        const float a = (float)(prs[j0(f) - 1] + (double)r0.y);
+        PllState q;
+        PllCtx c{};
+        pll_state_at(q, c, r0.x, r0.y, trig0, (long long)j0(f), a, DeviceLib{});
+        exact(q, c, kf, nb);
+    }
+#ifdef FMRX_AB_PROF
+    if (t == 0) {
+        atomicAdd(&g_pipe_prof[0], ch_body);
+        atomicAdd(&g_pipe_prof[1], ch_wait);
+        atomicAdd(&g_pipe_prof[4], (unsigned long long)ni);
+        atomicAdd(&g_pipe_prof[5], n_redo);
+    }
+#endif
+    (void)ch_body;
+    (void)ch_wait;
+    (void)n_redo;
+}
+
 }  // namespace
 
 #ifdef FMRX_AB_PROF
+static void print_pred_prof();
+static void reg_pred_prof() {
+    static const bool reg = [] { return std::atexit(print_pred_prof) == 0; }();
+    (void)reg;
+}
 static void print_pred_prof() {
     unsigned long long h[6] = {};
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pred_prof), sizeof h) == hipSuccess && h[4])
         std::fprintf(stderr, "pll_pred prof: batches %llu chain body %.1f wait %.1f, evaluator body %.1f wait %.1f "
                      "(shader cycles per batch)\n", h[4], (double)h[0] / h[4], (double)h[1] / h[4],
                      (double)h[2] / h[4], (double)h[3] / h[4]);
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pipe_prof), sizeof h) == hipSuccess && h[4])
+        std::fprintf(stderr, "pll_pipe prof: intervals %llu chain body %.1f wait %.1f, evaluator body %.1f wait %.1f "
+                     "(shader cycles per interval), %llu redos\n", h[4], (double)h[0] / h[4], (double)h[1] / h[4],
+                     (double)h[2] / h[4], (double)h[3] / h[4], h[5]);
 }
 #endif
 
 void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_streams, int spw, size_t stride,
                      const double* side, size_t seg, double step, float norm_bw, const float* st, float* out,
-                     size_t ostride, int* fail, float2* rec, size_t rb, int inject, int sat_ok) {
+                     size_t ostride, int* fail, float2* rec, size_t rb, int inject, int sat_ok, int pipe_on) {
 #ifdef FMRX_AB_PROF
-    static const bool reg = [] { return std::atexit(print_pred_prof) == 0; }();
-    (void)reg;
+    reg_pred_prof();
 #endif
     hipLaunchKernelGGL(pll_pred_kernel<kPllBatch>, dim3(waves), dim3(128), 0, s, io, n, n_streams, spw, stride, side,
-                       seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, sat_ok);
+                       seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, sat_ok, pipe_on);
+}
+
+void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_t stride, const double* side,
+                     size_t seg, double step, float norm_bw, const float* st, float* out, size_t ostride, int* fail,
+                     float2* rec, size_t rb, int inject) {
+#ifdef FMRX_AB_PROF
+    reg_pred_prof();
+#endif
+    hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams, stride,
+                       side, seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject);
 }
 
 }  // namespace fmrx

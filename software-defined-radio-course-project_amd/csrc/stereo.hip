@@ -934,18 +934,28 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     const dim3 grid((waves + wpg - 1) / wpg), block(64 * wpg);
 
     // filter.cpp:163: 2*PI*(freq/Fs) in double from the float quotient (host == device IEEE)
+    // FMRX_PLL_PIPE=0 (measurements, tests): no three-wave runner
+    const int pipe_env = [] {
+        const char* e = std::getenv("FMRX_PLL_PIPE");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+
     const double step = (2.0 * 3.14159265358979323846) * static_cast<double>(freq / fs);  // dy4.h:14 PI
     const bool step_ok = std::fabs(step * (double)kPllTrigStick) < kPllMaxPr;
     for (size_t off = 0; off < (size_t)n; off += seg) {
-        // the runners a segment can need (pll_sat_segment / pll_pred_wave take their waves, the
-        // lane kernel the rest): with known trigOffset bounds the others are not launched
+        // the runners a segment can need (pll_pipe_stream / pll_sat_segment / pll_pred_wave take
+        // their streams, the lane kernel the rest): with known trigOffset bounds the others are
+        // not launched.  The three-wave runner wants a SIMD per wave: one stream a workgroup
         const double lo = std::min(hint.trig_lo + (double)off, (double)kPllTrigStick);
         const double hi = std::min(hint.trig_hi + (double)off, (double)kPllTrigStick);
         const bool k = hint.known && step_ok;
-        const bool sat_all = k && sat_ok && spw == 1 && lo >= (double)kPllTrigStick;  // every wave saturated
+        const bool run_pipe = spec && pred_ok && pipe_env && spw == 1 && 3 * n_streams <= n_simd &&
+                              (!k || hi >= (double)kPllPipeMin);
+        const bool pipe_all = run_pipe && k && lo >= (double)kPllPipeMin;  // every stream to it
+        const bool sat_all = k && sat_ok && spw == 1 && !run_pipe && lo >= (double)kPllTrigStick;
         const bool run_lane = !(k && lo >= (double)kPllPredMin && (pred_ok || sat_all));
-        const bool run_sat = sat_ok && spw == 1 && (!k || hi >= (double)kPllTrigStick);
-        const bool run_pred = pred_ok && (!k || hi >= (double)kPllPredMin) && !sat_all;
+        const bool run_sat = sat_ok && spw == 1 && !run_pipe && (!k || hi >= (double)kPllTrigStick);
+        const bool run_pred = pred_ok && (!k || hi >= (double)kPllPredMin) && !sat_all && !pipe_all;
         const int m = (int)std::min(seg, (size_t)n - off);
         float* x = io + off;
         if (spw <= 4)  // the split kernels read stream-major side data
@@ -969,7 +979,11 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
                 // waves from trigOffset 2^20 below the stick (pll_pred_wave)
                 if (run_pred)
                     launch_pll_pred(waves, s, x, m, n_streams, spw, stride, side, seg, step, norm_bw, st, args, seg,
-                                    fail, rec, rb, inject, run_sat ? 1 : 0);
+                                    fail, rec, rb, inject, run_sat ? 1 : 0, run_pipe ? 1 : 0);
+                // one stream a workgroup from trigOffset 2^22 (pll_pipe_stream)
+                if (run_pipe)
+                    launch_pll_pipe(s, x, m, n_streams, stride, side, seg, step, norm_bw, st, args, seg, fail, rec,
+                                    rb, inject);
             } else
                 hipLaunchKernelGGL(pll_spec_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw,
                                    stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
