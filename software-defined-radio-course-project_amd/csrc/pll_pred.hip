@@ -393,26 +393,24 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
 // output goes through pll_check_kernel like every runner's.
 
 // The chain's candidate choice, e of trigArg_{j-1} from the phase: a = (T0, T1, e(c0 - 1),
-// e(c0)), ep = e(c0 + 1); phase < T0 -> c0 - 1, < T1 -> c0, else c0 + 1, by the sign bits of
-// the exact differences (arithmetic shifts to masks, bitfield inserts).  One asm block: as
-// separate statements the compiler pads each with a wait state, and left to itself it turns
-// the select into compare + v_cndmask (a VCC write and its wait states).
+// e(c0)), ep = e(c0 + 1); phase >= T1 -> c0 + 1, >= T0 -> c0, else c0 - 1.  One asm block: two
+// compares into SGPR masks, then the two v_cndmask, with the two wait states a VALU-written lane
+// mask needs before a VALU reads it (the s_nop and the first v_cndmask stand between each compare
+// and its reader).  Left to itself the compiler writes VCC twice, each with its own wait states;
+// as separate statements it pads each one (tools/ubench_chain.hip, modes 6 and 9).
 __device__ inline float pick(float phase, float4 a, float ep) {
     float e;
-    uint32_t d0, d1;
-    asm("v_sub_f32 %1, %3, %4\n"
-        "v_sub_f32 %2, %3, %5\n"
-        "v_ashrrev_i32 %1, 31, %1\n"
-        "v_ashrrev_i32 %2, 31, %2\n"
-        "v_bfi_b32 %1, %1, %6, %7\n"
-        "v_bfi_b32 %0, %2, %1, %8"
-        : "=&v"(e), "=&v"(d0), "=&v"(d1)
+    uint64_t m0, m1;
+    asm("v_cmp_ge_f32_e64 %1, %3, %4\n"
+        "v_cmp_ge_f32_e64 %2, %3, %5\n"
+        "s_nop 0\n"
+        "v_cndmask_b32_e64 %0, %6, %7, %1\n"
+        "v_cndmask_b32_e64 %0, %0, %8, %2"
+        : "=&v"(e), "=&s"(m0), "=&s"(m1)
         : "v"(phase), "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(ep));
     return e;
 }
 
-// NB-step batches (pll_check_kernel's), BPI of them an interval of NI = NB BPI steps: one
-// barrier an interval; RD intervals of step data in flight in the evaluators' load ring.
 // One wave a SIMD (amdgpu_waves_per_eu): the register budget is the chain's, so the scheduler
 // keeps each burst of reads whole instead of threading it through the steps for occupancy.
 template <int NB, int BPI, int RD>
