@@ -65,7 +65,7 @@ int main(int argc, char** argv) {
     }
     // ranges of j (step index = trigOffset - 1)
     const size_t edges[] = {0, 1u << 16, 1u << 20, 1u << 22, 1u << 23, 1u << 24, N};
-    const int batches[] = {1, 4, 8, 16};
+    const int batches[] = {1, 4, 8, 16, 32, 64, 128};
     // lookback: the candidate's phase is the one at the end of batch b - lb (lb = 1: the
     // previous batch; lb = 2 lets the candidates of batch b + 1 be evaluated during batch b)
     const int lb = argc > 2 ? std::atoi(argv[2]) : 1;
