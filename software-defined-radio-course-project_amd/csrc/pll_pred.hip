@@ -417,7 +417,7 @@ template <int NB, int BPI, int RD>
 __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))) pll_pipe_kernel(const float* io, int n, int n_streams, size_t stride,
                                                       const double* side, size_t seg, double step, float norm_bw,
                                                       const float* st, float* out_base, size_t ostride, int* fail,
-                                                      float2* rec, size_t rb, int inject) {
+                                                      float2* rec, size_t rb, int inject, int miss) {
     constexpr int NI = NB * BPI;
     static_assert(NI == 32 || NI == 64, "the evaluators' lane map: 64 / NI lanes a step");
     constexpr int LPS = 64 / NI;  // evaluator lanes a step
@@ -524,6 +524,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             const bool bad = (__builtin_bit_cast(uint32_t, a) - cm > 2u) || !(tt.x > -__builtin_inff()) ||
                              !(tt.y > -__builtin_inff()) || !(c0 > 0.0f && c0 < 3.0e38f);
             bool any = __builtin_amdgcn_ballot_w64(bad) != 0;
+            if (k == min(miss, ni)) any = true;  // test hook: a miss on interval `miss` (the redo path)
 #ifdef FMRX_AB_NOREAD
             any = false;
 #endif
@@ -753,12 +754,12 @@ void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_str
 
 void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_t stride, const double* side,
                      size_t seg, double step, float norm_bw, const float* st, float* out, size_t ostride, int* fail,
-                     float2* rec, size_t rb, int inject) {
+                     float2* rec, size_t rb, int inject, int miss) {
 #ifdef FMRX_AB_PROF
     reg_pred_prof();
 #endif
     hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams, stride,
-                       side, seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject);
+                       side, seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, miss);
 }
 
 }  // namespace fmrx

@@ -934,10 +934,15 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     const dim3 grid((waves + wpg - 1) / wpg), block(64 * wpg);
 
     // filter.cpp:163: 2*PI*(freq/Fs) in double from the float quotient (host == device IEEE)
-    // FMRX_PLL_PIPE=0 (measurements, tests): no three-wave runner
+    // FMRX_PLL_PIPE=0 (measurements, tests): no three-wave runner; FMRX_PLL_PIPE_MISS=k (test
+    // hook): its check reports a miss on interval k of every segment, so the redo path runs
     const int pipe_env = [] {
         const char* e = std::getenv("FMRX_PLL_PIPE");
         return (e && e[0] == '0') ? 0 : 1;
+    }();
+    const int pipe_miss = [] {
+        const char* e = std::getenv("FMRX_PLL_PIPE_MISS");
+        return e ? std::atoi(e) : -1;
     }();
 
     const double step = (2.0 * 3.14159265358979323846) * static_cast<double>(freq / fs);  // dy4.h:14 PI
@@ -983,7 +988,7 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
                 // one stream a workgroup from trigOffset 2^22 (pll_pipe_stream)
                 if (run_pipe)
                     launch_pll_pipe(s, x, m, n_streams, stride, side, seg, step, norm_bw, st, args, seg, fail, rec,
-                                    rb, inject);
+                                    rb, inject, pipe_miss);
             } else
                 hipLaunchKernelGGL(pll_spec_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw,
                                    stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);

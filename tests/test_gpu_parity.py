@@ -700,14 +700,16 @@ def test_pll_primitive_states(fmrx, orc, trig, phase, freq, fs, n, offset):
 
 @pytest.mark.parametrize("freq,nco_scale", [(19000, 2.0), (114000, 0.5)])  # pilot (project.cpp:166), RDS (:226)
 @pytest.mark.parametrize("inject", [None, "3"])
-@pytest.mark.parametrize("sat", ["1", "0"])
-def test_pll_saturated_runner(fmrx, orc, monkeypatch, inject, sat, freq, nco_scale):
+@pytest.mark.parametrize("sat,pipe", [("1", "1"), ("1", "0"), ("0", "0")])
+def test_pll_saturated_runner(fmrx, orc, monkeypatch, inject, sat, pipe, freq, nco_scale):
     """A segment that starts with trigOffset stuck at 2^24 (filter.cpp:165-166 in float, 69.9 s
-    into a stream): the saturated-segment runner (pll_sat.hip; FMRX_PLL_SAT=0: the ordinary
-    one), and a corrupted runner batch (check + certified resume).  The
+    into a stream): the three-wave runner (pll_pred.hip pll_pipe_kernel, which takes one stream
+    a workgroup), with it off the saturated-segment runner (pll_sat.hip), with both off the
+    two-wave predicted runner; and a corrupted runner batch (check + certified resume).  The
     speculation counters must show every batch verified without the corruption -- a runner
     that disagrees with the exact path would otherwise pass here, fixed up by the resume."""
     monkeypatch.setenv("FMRX_PLL_SAT", sat)
+    monkeypatch.setenv("FMRX_PLL_PIPE", pipe)
     if inject is not None:
         monkeypatch.setenv("FMRX_PLL_SPEC_INJECT", inject)
     n = 20000
@@ -734,13 +736,16 @@ def test_pll_saturated_runner(fmrx, orc, monkeypatch, inject, sat, freq, nco_sca
 
 @pytest.mark.parametrize("trig0", [1048576.0, 4194321.0, 16772216.0, 1048575.0])
 @pytest.mark.parametrize("inject", [None, "5"])
-@pytest.mark.parametrize("pred", ["1", "0"])
-def test_pll_predicted_runner(fmrx, orc, monkeypatch, trig0, inject, pred):
-    """Segments from trigOffset 2^20 up to the 2^24 stick: the predicted-trigArg runner
-    (pll_pred.hip; FMRX_PLL_PRED=0: the lane runner), starting at 2^20, at 2^22 + 17, and 5,000
-    steps below the stick (its pr stops rising inside the segment); 2^20 - 1 stays on the lane
-    runner.  A corrupted batch must be caught and resumed; without it every batch verifies."""
+@pytest.mark.parametrize("pred,pipe", [("1", "1"), ("1", "0"), ("0", "0")])
+def test_pll_predicted_runner(fmrx, orc, monkeypatch, trig0, inject, pred, pipe):
+    """Segments from trigOffset 2^20 up to the 2^24 stick: the predicted-trigArg runners
+    (pll_pred.hip: two waves from 2^20, three waves one stream a workgroup from 2^22;
+    FMRX_PLL_PIPE=0: the two-wave one throughout; FMRX_PLL_PRED=0: the lane runner), starting at
+    2^20, at 2^22 + 17, and 5,000 steps below the stick (its pr stops rising inside the segment);
+    2^20 - 1 stays on the lane runner.  A corrupted batch must be caught and resumed; without it
+    every batch verifies."""
     monkeypatch.setenv("FMRX_PLL_PRED", pred)
+    monkeypatch.setenv("FMRX_PLL_PIPE", pipe)
     if inject is not None:
         monkeypatch.setenv("FMRX_PLL_SPEC_INJECT", inject)
     n = 20000
@@ -763,6 +768,64 @@ def test_pll_predicted_runner(fmrx, orc, monkeypatch, trig0, inject, pred):
         resumed, checked = counts.cpu().tolist()
         assert checked == n // 16
         assert (resumed > 0) if inject is not None else (resumed == 0), (resumed, checked)
+
+
+@pytest.mark.parametrize("trig0", [4194321.0, 16772216.0, 16777216.0])
+@pytest.mark.parametrize("miss", ["1", "2", "150", "311", "312", "5000"])
+def test_pll_pipe_redo(fmrx, orc, monkeypatch, trig0, miss):
+    """The three-wave runner's miss path (pll_pipe_kernel): FMRX_PLL_PIPE_MISS=k makes its check
+    report interval k as missed (past the last interval: the last), so the chain redoes that
+    interval and the two after it exactly and the evaluators restart from the corrected phase.
+    20,000 steps = batch 0 + 312 intervals of 64 steps + 1 batch: k = 1 (the first), 150, 311
+    and 312 (the verdicts read after the loop).  Bit-exact, and every batch verifies."""
+    monkeypatch.setenv("FMRX_PLL_PIPE_MISS", miss)
+    n = 20000
+    rng = np.random.default_rng(int(trig0) % 977)
+    t = np.arange(n)
+    x = (0.1 * np.cos(2 * np.pi * 19000 / 240000 * t + 0.2) + 0.005 * rng.standard_normal(n)).astype(np.float32)
+    st0 = np.array([1e-4, 0.4, 0.6, 0.8, 1.0, trig0], np.float32)
+    want_x, want_st = orc.pll(x, 19000, 240000, 2.0, 0.0, 0.01, st0)
+    with fmrx.Receiver(0, fmrx.STEREO) as rx:
+        buf = _d(x)
+        st = _d(st0)
+        counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+        rx.debug_pll_stats(counts.data_ptr())
+        torch.cuda.synchronize()
+        rx.pll(buf.data_ptr(), n, 19000, 240000, 2.0, 0.0, 0.01, st.data_ptr())
+        rx.synchronize()
+        rx.debug_pll_stats(None)
+        assert same(buf.cpu().numpy(), want_x)
+        assert same(st.cpu().numpy(), want_st)
+        resumed, checked = counts.cpu().tolist()
+        assert checked == n // 16 and resumed == 0, (resumed, checked)
+
+
+def test_pipe_runner_streams(fmrx, monkeypatch):
+    """pll_pipe_kernel over many streams (300: three waves each still fit the SIMDs), every
+    stream put at its own trigOffset in [2^22, 2^22 + 300) through the state blob, 24 blocks in one
+    call: every batch verifies, and the PCM equals the same call with the three-wave runner off
+    (FMRX_PLL_PIPE=0: the two-wave runner; both are checked by pll_check_kernel)."""
+    ns, nb, bb = 300, 24, 12800
+    ins = np.stack([iqgen.make("synth:%d" % (900 + s % 7), (nb + 2) * bb) for s in range(ns)])
+    outs = []
+    for pipe in ("1", "0"):
+        monkeypatch.setenv("FMRX_PLL_PIPE", pipe)
+        with fmrx.Receiver(0, fmrx.STEREO, n_streams=ns) as rx:
+            rx.process(ins[:, : 2 * bb])
+            blob = bytearray(rx.get_state())
+            hdr = np.frombuffer(bytes(blob[:40]), np.uint32)
+            pll_off = 40 + ns * (int(hdr[6]) + 4 * int(hdr[7]) + 4 * 64)
+            pll = np.frombuffer(bytes(blob[pll_off: pll_off + ns * 32]), np.float32).reshape(ns, 8).copy()
+            pll[:, 5] = 4194304.0 + np.arange(ns, dtype=np.float32)
+            blob[pll_off: pll_off + ns * 32] = pll.tobytes()
+            rx.set_state(bytes(blob))
+            counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+            rx.debug_pll_stats(counts.data_ptr())
+            outs.append(rx.process(ins[:, 2 * bb:]))
+            rx.debug_pll_stats(None)
+        resumed, checked = counts.cpu().tolist()
+        assert checked > 0 and resumed == 0, (pipe, resumed, checked)
+    assert np.array_equal(outs[0], outs[1])
 
 
 def test_predicted_runner_rows(fmrx):
