@@ -100,6 +100,25 @@ __device__ inline float phase_thr(double P, uint32_t cb) {
     return (rp && !rmm) ? T : -__builtin_inff();
 }
 
+// The chain's candidate choice, e of trigArg_{j-1} from the phase: a = (T0, T1, e(c0 - 1),
+// e(c0)), ep = e(c0 + 1); phase >= T1 -> c0 + 1, >= T0 -> c0, else c0 - 1.  One asm block: two
+// compares into SGPR masks, then the two v_cndmask, with the two wait states a VALU-written lane
+// mask needs before a VALU reads it (the s_nop and the first v_cndmask stand between each compare
+// and its reader).  Left to itself the compiler writes VCC twice, each with its own wait states;
+// as separate statements it pads each one (tools/ubench_chain.hip, modes 6 and 9).
+__device__ inline float pick(float phase, float4 a, float ep) {
+    float e;
+    uint64_t m0, m1;
+    asm("v_cmp_ge_f32_e64 %1, %3, %4\n"
+        "v_cmp_ge_f32_e64 %2, %3, %5\n"
+        "s_nop 0\n"
+        "v_cndmask_b32_e64 %0, %6, %7, %1\n"
+        "v_cndmask_b32_e64 %0, %0, %8, %2"
+        : "=&v"(e), "=&s"(m0), "=&s"(m1)
+        : "v"(phase), "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(ep));
+    return e;
+}
+
 template <int NB>
 __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, int n_streams, int spw, size_t stride,
                                                       const double* side, size_t seg, double step, float norm_bw,
@@ -303,7 +322,7 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
                 float4 a, bb;
                 sel_of(jc, a, bb);
                 // the chain: two compares of the phase, e, (Ki e, Kp e), the three float updates
-                const float e = phase >= a.y ? bb.y : (phase >= a.x ? bb.x : a.w);
+                const float e = pick(phase, make_float4(a.x, a.y, a.w, bb.x), bb.y);
                 const float2v k = float2v{Ki, Kp} * e;
                 integ = integ + k.x;
                 phase = phase + (k.y + integ);
@@ -326,7 +345,7 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
                     constexpr int J = decltype(jc)::value;
                     float4 a, bb;
                     sel_of(jc, a, bb);
-                    float e = phase >= a.y ? bb.y : (phase >= a.x ? bb.x : a.w);
+                    float e = pick(phase, make_float4(a.x, a.y, a.w, bb.x), bb.y);
                     if (__builtin_bit_cast(uint32_t, tprev) - __builtin_bit_cast(uint32_t, a.z) > 2u)
                         e = pred_e(tprev, x[j0 + J], ivs[j0 + J]);
                     const float2v k = float2v{Ki, Kp} * e;
@@ -392,25 +411,6 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
 // candidates held on every step of the bench stream (tools/pll_predict.cpp), so this is rare; the
 // output goes through pll_check_kernel like every runner's.
 
-// The chain's candidate choice, e of trigArg_{j-1} from the phase: a = (T0, T1, e(c0 - 1),
-// e(c0)), ep = e(c0 + 1); phase >= T1 -> c0 + 1, >= T0 -> c0, else c0 - 1.  One asm block: two
-// compares into SGPR masks, then the two v_cndmask, with the two wait states a VALU-written lane
-// mask needs before a VALU reads it (the s_nop and the first v_cndmask stand between each compare
-// and its reader).  Left to itself the compiler writes VCC twice, each with its own wait states;
-// as separate statements it pads each one (tools/ubench_chain.hip, modes 6 and 9).
-__device__ inline float pick(float phase, float4 a, float ep) {
-    float e;
-    uint64_t m0, m1;
-    asm("v_cmp_ge_f32_e64 %1, %3, %4\n"
-        "v_cmp_ge_f32_e64 %2, %3, %5\n"
-        "s_nop 0\n"
-        "v_cndmask_b32_e64 %0, %6, %7, %1\n"
-        "v_cndmask_b32_e64 %0, %0, %8, %2"
-        : "=&v"(e), "=&s"(m0), "=&s"(m1)
-        : "v"(phase), "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(ep));
-    return e;
-}
-
 // One wave a SIMD (amdgpu_waves_per_eu): the register budget is the chain's, so the scheduler
 // keeps each burst of reads whole instead of threading it through the steps for occupancy.
 template <int NB, int BPI, int RD>
@@ -419,9 +419,9 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                                                       const float* st, float* out_base, size_t ostride, int* fail,
                                                       float2* rec, size_t rb, int inject, int miss) {
     constexpr int NI = NB * BPI;
-    static_assert(NI == 32 || NI == 64, "the evaluators' lane map: 64 / NI lanes a step");
-    constexpr int LPS = 64 / NI;  // evaluator lanes a step
-    constexpr int CH = 32;        // the chain's steps a burst of reads
+    static_assert(NI == 16 || NI == 32 || NI == 64, "the evaluators' lane map: 64 / NI lanes a step");
+    constexpr int LPS = 64 / NI;             // evaluator lanes a step
+    constexpr int CH = NI < 32 ? NI : 32;    // the chain's steps a burst of reads
     // rings of four intervals (interval k in slot k & 3; interval 0 is batch 0): per step the
     // thresholds T0, T1 and the e of c0 - 1 ulp and c0 (sel), the e of c0 + 1 ulp (sep),
     // bits(c0) - 1 (scb), P (spr); the chain's phases (sph); per interval the check's verdict
@@ -440,7 +440,11 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     const float Kp = norm_bw * static_cast<float>(2.666);
     const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
     PllState p{S[0], S[1], S[2], S[3], S[5]};
-    if (!pll_pipe_stream(p.trig, step)) return;  // uniform over the group
+    // the interval length's domain (uniform over the group): 64-step intervals from 2^22, 16-step
+    // ones in [2^21, 2^22)
+    if (!(NI == 64 ? pll_pipe_stream(p.trig, step, kPllPipeMin)
+                   : pll_pipe_stream(p.trig, step, kPllPipeMin16, kPllPipeMin - 1.0f)))
+        return;
     const float trig0 = p.trig;
     const int nb = n / NB;
     const int ni = (nb - 1) / BPI;  // intervals after batch 0
@@ -525,7 +529,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                              !(tt.y > -__builtin_inff()) || !(c0 > 0.0f && c0 < 3.0e38f);
             bool any = __builtin_amdgcn_ballot_w64(bad) != 0;
             if (k == min(miss, ni)) any = true;  // test hook: a miss on interval `miss` (the redo path)
-#ifdef FMRX_AB_NOREAD
+#if defined(FMRX_AB_NOREAD) || defined(FMRX_AB_NOSTORE)
             any = false;
 #endif
             if (l == 0) smiss[sl] = any ? 1 : 0;
@@ -653,7 +657,15 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                         brec[CH / NB - 1].y = phase;
                     }
                 }
+                // Every read of the burst has landed by now (the steps used them), but the waitcnt
+                // pass cannot tell: after the stores' exec-masked branch it would wait for the
+                // stores too (lgkmcnt(0)) before the next burst's first use.  Waiting here is free.
+                __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+#ifdef FMRX_AB_NOSTORE  // A/B timing only (wrong results): no phase or record stores
+                if (t == 0 && phase == 12345.0f) {
+#else
                 if (t == 0) {
+#endif
 #pragma unroll
                     for (int q = 0; q < CH / 4; q++)
                         reinterpret_cast<float4*>(&sph[is][H * CH])[q] = *reinterpret_cast<const float4*>(&PH[4 * q]);
@@ -754,12 +766,16 @@ void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_str
 
 void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_t stride, const double* side,
                      size_t seg, double step, float norm_bw, const float* st, float* out, size_t ostride, int* fail,
-                     float2* rec, size_t rb, int inject, int miss) {
+                     float2* rec, size_t rb, int inject, int miss, bool long_iv, bool short_iv) {
 #ifdef FMRX_AB_PROF
     reg_pred_prof();
 #endif
-    hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams, stride,
-                       side, seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, miss);
+    if (long_iv)
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
+                           stride, side, seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, miss);
+    if (short_iv)
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 1, 8>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
+                           stride, side, seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, miss);
 }
 
 }  // namespace fmrx

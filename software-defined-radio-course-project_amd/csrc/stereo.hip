@@ -955,8 +955,10 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         const double hi = std::min(hint.trig_hi + (double)off, (double)kPllTrigStick);
         const bool k = hint.known && step_ok;
         const bool run_pipe = spec && pred_ok && pipe_env && spw == 1 && 3 * n_streams <= n_simd &&
-                              (!k || hi >= (double)kPllPipeMin);
-        const bool pipe_all = run_pipe && k && lo >= (double)kPllPipeMin;  // every stream to it
+                              (!k || hi >= (double)kPllPipeMin16);
+        const bool pipe_all = run_pipe && k && lo >= (double)kPllPipeMin16;  // every stream to it
+        const bool pipe_long = run_pipe && (!k || hi >= (double)kPllPipeMin);
+        const bool pipe_short = run_pipe && (!k || lo < (double)kPllPipeMin);
         const bool sat_all = k && sat_ok && spw == 1 && !run_pipe && lo >= (double)kPllTrigStick;
         const bool run_lane = !(k && lo >= (double)kPllPredMin && (pred_ok || sat_all));
         const bool run_sat = sat_ok && spw == 1 && !run_pipe && (!k || hi >= (double)kPllTrigStick);
@@ -985,10 +987,10 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
                 if (run_pred)
                     launch_pll_pred(waves, s, x, m, n_streams, spw, stride, side, seg, step, norm_bw, st, args, seg,
                                     fail, rec, rb, inject, run_sat ? 1 : 0, run_pipe ? 1 : 0);
-                // one stream a workgroup from trigOffset 2^22 (pll_pipe_stream)
+                // one stream a workgroup from trigOffset 2^21 (pll_pipe_stream)
                 if (run_pipe)
                     launch_pll_pipe(s, x, m, n_streams, stride, side, seg, step, norm_bw, st, args, seg, fail, rec,
-                                    rb, inject, pipe_miss);
+                                    rb, inject, pipe_miss, pipe_long, pipe_short);
             } else
                 hipLaunchKernelGGL(pll_spec_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw,
                                    stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);

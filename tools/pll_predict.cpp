@@ -64,7 +64,7 @@ int main(int argc, char** argv) {
         fbQ = (float)std::sin((double)a);
     }
     // ranges of j (step index = trigOffset - 1)
-    const size_t edges[] = {0, 1u << 16, 1u << 20, 1u << 22, 1u << 23, 1u << 24, N};
+    const size_t edges[] = {0, 1u << 16, 1u << 20, 1u << 21, 1u << 22, 1u << 23, 1u << 24, N};
     const int batches[] = {1, 4, 8, 16, 32, 64, 128};
     // lookback: the candidate's phase is the one at the end of batch b - lb (lb = 1: the
     // previous batch; lb = 2 lets the candidates of batch b + 1 be evaluated during batch b)
@@ -78,7 +78,7 @@ int main(int argc, char** argv) {
     std::printf("phase range [%g, %g]\n", pmin, pmax);
     std::printf("%-22s %5s %9s %9s %9s %9s %12s\n", "j range", "B", "k=0", "|k|<=1", "|k|<=2", "|k|>2",
                 "batch|k|<=1");
-    for (int r = 0; r + 1 < 7; r++) {
+    for (int r = 0; r + 1 < 8; r++) {
         const size_t j0 = edges[r], j1 = std::min(edges[r + 1], N);
         if (j0 >= j1) continue;
         for (int B : batches) {
@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
     // two candidates: c0 and its neighbour on the side of the exact sum P + phase_ref (the
     // rounding's direction), batches of B with lookback lb
     std::printf("two candidates (c0 and the neighbour towards P + phase_ref):\n");
-    for (int r = 2; r + 1 < 7; r++) {
+    for (int r = 2; r + 1 < 8; r++) {
         const size_t j0 = edges[r], j1 = std::min(edges[r + 1], N);
         if (j0 >= j1) continue;
         for (int B : {8, 16}) {
