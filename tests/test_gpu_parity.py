@@ -831,11 +831,14 @@ def test_pipe_runner_streams(fmrx, monkeypatch):
     assert np.array_equal(outs[0], outs[1])
 
 
-def test_predicted_runner_rows(fmrx):
-    """pll_pred.hip with two streams a wave (1,100 streams: 16-lane rows), every stream put at
-    its own trigOffset in [2^21, 2^21 + 1100) through the state blob -- except stream 5, at
-    1,000, which sends its wave (streams 4 and 5) to the lane runner -- 40 blocks in one call,
-    every batch verified, and streams on both sides compared with the same stream alone."""
+def test_predicted_runner_rows(fmrx, monkeypatch):
+    """pll_pred.hip with two streams a wave (1,100 streams: 16-lane rows; FMRX_PLL_PRED=2 launches
+    it although its 550 two-wave groups would share SIMDs, where the host leaves such counts to
+    the lane runner), every stream put at its own trigOffset in [2^21, 2^21 + 1100) through the
+    state blob -- except stream 5, at 1,000, which sends its wave (streams 4 and 5) to the lane
+    runner -- 40 blocks in one call, every batch verified, and streams on both sides compared
+    with the same stream alone."""
+    monkeypatch.setenv("FMRX_PLL_PRED", "2")
     ns, nb, bb = 1100, 40, 12800
     ins = np.stack([iqgen.make("synth:%d" % (700 + s % 5), (nb + 2) * bb) for s in range(ns)])
     with fmrx.Receiver(0, fmrx.STEREO, n_streams=ns) as rx:
