@@ -45,7 +45,7 @@ def kernel_name() -> str:
     return _VARIANTS[int(os.environ.get("FMRX_MONO_VARIANT", "6"))]  # csrc kDefaultVariant
 
 
-KERNEL_SOURCES = ("mono_fused.hip", "dsp_device.h", "fmrx_internal.h")
+KERNEL_SOURCES = ("mono_fused.hip", "dsp_device.h", "mono_launch.h")
 
 
 def kernel_source_hash() -> str:

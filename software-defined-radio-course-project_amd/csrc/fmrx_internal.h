@@ -5,6 +5,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "mono_launch.h"
 #include "synth.h"
 
 namespace fmrx {
@@ -17,58 +18,10 @@ bool mode_constants(int mode, ModeConstants* m);
 void design_lpf(float* h, float fs, float fc, int taps, int gain);
 void design_bpf(float* h, float fs, float fb, float fe, int taps);
 
-constexpr int kMaxRfTaps = 256;
 constexpr int kMonoDelay = 5;   // src/project.cpp:308
 constexpr int kRfFc = 100000;   // src/project.cpp:304
 constexpr int kAudioFc = 16000; // src/project.cpp:305
 
-constexpr int kMaxAudioTaps = 64;
-constexpr int kAudioRow = 52;   // one polyphase phase of the 51-taps-per-phase audio prototype, 16-B rows
-
-// Coefficient tables handed to kernels by value (kernarg segment -> scalar registers).
-struct MonoTaps {
-    float rf[kMaxRfTaps];
-    float audio[kMaxAudioTaps];
-};
-
-// ---- fused mono receiver (a1 a4 a5 a6 a12; MONO semantics) ---------------------------
-struct MonoLaunch {
-    const uint8_t* iq;          // n_streams x stream_bytes
-    const uint8_t* halo;        // n_streams x halo_bytes: bytes preceding this call
-    int16_t* pcm;               // n_streams x n_blocks*audio_frames
-    float* mono;                // optional float output (same shape), may be null
-    float* demod;               // optional demod output, written at demod[s*demod_stride +
-                                //   demod_hist + g] for IF index g (stereo engine input)
-    size_t demod_stride;
-    int demod_hist;
-    float* demod_tail;          // optional: the last AH demod samples, at demod_tail +
-                                //   s * demod_tail_stride for stream s
-    size_t demod_tail_stride;
-    const float* audio_coeff;   // modes 2/3: the rational resampler's prototype (device)
-    const float* audio_rows;    // modes 2/3: the same taps as `up` rows of kAudioRow floats,
-                                //   row k0 = coeff[k0 + i up] for i < 51 (then zeros)
-    size_t stream_bytes;        // n_blocks * block_bytes
-    size_t halo_bytes;
-    long long n_if;             // IF samples per stream this call
-    int segs;                   // workgroups (segments) per stream
-    int audio;                  // 1: run the audio stage (pcm / mono outputs)
-    unsigned long long* stamps; // diagnostic (fmrx_debug_mono_stamps): 6 u64 per workgroup, else null
-    int older_share;            // 0: equal segments; else (even segs, two waves per SIMD) the
-                                //   first-dispatched wave's share of a SIMD's span, in 1/1024
-    uint8_t* halo_next;         // optional: the halo after this call (last halo_bytes of halo ++
-                                //   iq per stream), written by the kernel in 16-B words; the
-                                //   caller guarantees 16-B aligned iq rows (else null + halo_kernel)
-};
-
-// Halo bytes the fused kernel needs in front of a call (pre-roll chunk + RF history).
-size_t mono_halo_bytes(int rf_taps, int rf_decim, int audio_down);
-// Chunks (work units) per stream for n_if IF samples, used to size the grid.
-long long mono_chunks(long long n_if, int rf_taps, int rf_decim, int audio_down);
-// Resident workgroups per CU of the selected variant (grid sizing).
-int mono_wg_per_cu(int rf_decim);
-// Returns 0 on success, FMRX_EINVAL if no compiled variant matches.
-int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_decim,
-                      int audio_up, int audio_down, const MonoTaps& taps, hipStream_t s);
 // Halo bookkeeping: new_halo = last halo_bytes of (old_halo ++ iq), per stream.
 int launch_halo_update(const uint8_t* iq, size_t stream_bytes, const uint8_t* old_halo,
                        uint8_t* new_halo, size_t halo_bytes, int n_streams, hipStream_t s);

@@ -34,7 +34,7 @@
 #include <cstdlib>
 
 #include "dsp_device.h"
-#include "fmrx_internal.h"
+#include "mono_launch.h"
 
 namespace fmrx {
 
