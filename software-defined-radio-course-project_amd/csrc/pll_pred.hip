@@ -660,7 +660,11 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 // Every read of the burst has landed by now (the steps used them), but the waitcnt
                 // pass cannot tell: after the stores' exec-masked branch it would wait for the
                 // stores too (lgkmcnt(0)) before the next burst's first use.  Waiting here is free.
+                // (sched_barrier: the wait stays after the steps; the scheduler moves a bare
+                // s_waitcnt up among the burst's first steps)
+                __builtin_amdgcn_sched_barrier(0);
                 __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+                __builtin_amdgcn_sched_barrier(0);
 #ifdef FMRX_AB_NOSTORE  // A/B timing only (wrong results): no phase or record stores
                 if (t == 0 && phase == 12345.0f) {
 #else

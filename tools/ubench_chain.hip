@@ -14,6 +14,9 @@
 //   mode 9: mode 6 with the choice by two compares to SGPR masks and two v_cndmask,
 //   mode 10: mode 6 with the whole step in one asm block (choice, v_pk_mul, the three adds),
 //   mode 11: mode 10 with mode 9's choice,
+//   mode 12: mode 9 + the phases stored to LDS after the batch from lane 0 (exec-masked branch),
+//   mode 13: mode 9 + each group of 4 phases stored as soon as made, every lane to one address,
+//   mode 14: mode 9 + each group of 4 phases stored as soon as made, lane 0 only (exec in asm),
 // and the other waves (0, 1 or 2 of them) either idle at the barrier or busy with f64 FMAs
 // (`busy`); one barrier per batch when there are other waves.  Prints shader cycles per step.
 //
@@ -67,6 +70,7 @@ template <int MODE>
 __global__ void __launch_bounds__(192) chain(float* out, long long* cyc, int nb, int busy) {
     __shared__ float4 sel[2][NB];
     __shared__ float sep[2][NB];
+    __shared__ float4 sph[2][NB / 4];
     const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
     const int nw = blockDim.x >> 6;
     if (threadIdx.x < 2 * NB) {
@@ -136,6 +140,7 @@ __global__ void __launch_bounds__(192) chain(float* out, long long* cyc, int nb,
                 }
                 const float4 a = (MODE == 0 || MODE == 6 || MODE >= 9) ? A0[J] : A[J];
                 const float ep = (MODE == 0 || MODE == 6 || MODE >= 9) ? E0[J] : EP[J];
+                (void)0;
                 float e;
                 if constexpr (MODE == 10 || MODE == 11) {
                     uint32_t d0, d1;
@@ -159,7 +164,7 @@ __global__ void __launch_bounds__(192) chain(float* out, long long* cyc, int nb,
                             : "s40", "s41", "s42", "s43");
                     PH[J] = phase;
                     (void)e;
-                } else if constexpr (MODE == 9) {
+                } else if constexpr (MODE == 9 || MODE >= 12) {
                     asm volatile(
                         "v_cmp_ge_f32_e64 s[40:41], %1, %2\n v_cmp_ge_f32_e64 s[42:43], %1, %3\n s_nop 0\n"
                         " v_cndmask_b32_e64 %0, %4, %5, s[40:41]\n v_cndmask_b32_e64 %0, %0, %6, s[42:43]"
@@ -182,9 +187,27 @@ __global__ void __launch_bounds__(192) chain(float* out, long long* cyc, int nb,
                     phase = phase + (k.y + integ);
                     PH[J] = phase;
                 }
+                if constexpr ((MODE == 13 || MODE == 14) && J % 4 == 3) {
+                    const float4 v4 = make_float4(PH[J - 3], PH[J - 2], PH[J - 1], PH[J]);
+                    if constexpr (MODE == 13) {
+                        sph[b & 1][J / 4] = v4;
+                    } else {
+                        f4 v = {v4.x, v4.y, v4.z, v4.w};
+                        const unsigned a = (unsigned)(uintptr_t)&sph[b & 1][J / 4];
+                        asm volatile("s_mov_b64 s[44:45], exec\n s_mov_b64 exec, 1\n ds_write_b128 %0, %1\n"
+                                     " s_mov_b64 exec, s[44:45]" ::"v"(a), "v"(v) : "s44", "s45", "memory");
+                    }
+                }
                 if constexpr (MODE == 2 || MODE == 3) __builtin_amdgcn_sched_barrier(0);
             },
             std::make_integer_sequence<int, NB>{});
+        if constexpr (MODE == 12) {
+            if (t == 0) {
+#pragma unroll
+                for (int q = 0; q < NB / 4; q++)
+                    sph[b & 1][q] = make_float4(PH[4 * q], PH[4 * q + 1], PH[4 * q + 2], PH[4 * q + 3]);
+            }
+        }
 #pragma unroll
         for (int J = 0; J < NB; J++) acc += PH[J];
         phase = phase * 0.5f;  // keep it in range
@@ -238,6 +261,9 @@ int main() {
             run<9>(waves, busy, d_out, d_cyc);
             run<10>(waves, busy, d_out, d_cyc);
             run<11>(waves, busy, d_out, d_cyc);
+            run<12>(waves, busy, d_out, d_cyc);
+            run<13>(waves, busy, d_out, d_cyc);
+            run<14>(waves, busy, d_out, d_cyc);
         }
     }
     (void)hipFree(d_out);
