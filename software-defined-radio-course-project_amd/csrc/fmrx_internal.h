@@ -71,14 +71,15 @@ void launch_pll_sat(dim3 grid, dim3 block, hipStream_t s, const float* io, int n
 void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_streams, int spw, size_t stride,
                      const double* side, size_t seg, double step, float norm_bw, const float* st, float* out,
                      size_t ostride, int* fail, float2* rec, size_t rb, int inject, int sat_ok, int pipe_on);
-// pll_pred.hip: the three-wave runner for one stream a workgroup (spw == 1) from trigOffset 2^21,
-// the stick included (pll_pipe_stream): `long_iv` launches its 64-step-interval form for the
-// streams from 2^22, `short_iv` its 16-step form for those in [2^21, 2^22); launched, they take
-// those streams from the pred and saturated runners.  miss >= 1 (test hook): the check reports a
-// miss on that interval (the last one if past it), so the exact redo runs
+// pll_pred.hip: the three-wave runner for one stream a workgroup (spw == 1) from trigOffset 2^20,
+// the stick included (pll_pipe_stream): `from22` launches its form for the streams from 2^22 (3
+// candidates, 64-step intervals), `from21` the one for [2^21, 2^22) (5 candidates, 64 steps),
+// `from20` the one for [2^20, 2^21) (5 candidates, 16 steps); launched, they take those streams
+// from the pred and saturated runners.  miss >= 1 (test hook): the check reports a miss on that
+// interval (the last one if past it), so the exact redo runs
 void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_t stride, const double* side,
                      size_t seg, double step, float norm_bw, const float* st, float* out, size_t ostride, int* fail,
-                     float2* rec, size_t rb, int inject, int miss, bool long_iv, bool short_iv);
+                     float2* rec, size_t rb, int inject, int miss, bool from22, bool from21, bool from20);
 
 // test hook: the PLL's fallback libm on device (kind 0 sincos, 1 atan2, 2 NCO cos)
 int launch_pll_fallback_test(int kind, const float* a, const float* b, size_t n, float* out, hipStream_t s);

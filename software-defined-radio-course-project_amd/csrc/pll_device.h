@@ -105,14 +105,16 @@ __device__ inline bool pll_pred_wave(float trig0, double step) {
     return __builtin_amdgcn_ballot_w64(!ok) == 0;
 }
 
-// A stream for pll_pipe_kernel (one stream a workgroup, spw == 1): trigOffset in [2^21, 2^24] at
-// the segment start.  From 2^22 (kPllPipeMin) its 64-step intervals: every predicted trigArg of
-// the bench stream hit its three candidates there (tools/pll_predict.cpp); in [2^21, 2^22) 16-step
-// intervals, where 99.8 % of the batches hit (a miss costs an exact redo).  pll_pred_kernel and
-// pll_sat_kernel leave these streams to it when it is launched.
-constexpr float kPllPipeMin = 4194304.0f;    // 2^22
-constexpr float kPllPipeMin16 = 2097152.0f;  // 2^21
-__device__ inline bool pll_pipe_stream(float trig0, double step, float lo = kPllPipeMin16,
+// A stream for pll_pipe_kernel (one stream a workgroup, spw == 1): trigOffset in [2^20, 2^24] at
+// the segment start, where the predicted trigArgs of the bench stream hit their candidates
+// (tools/pll_predict.cpp): three candidates in 64-step intervals from 2^22 (every interval), five
+// in 64-step intervals in [2^21, 2^22) (99.97 %), five in 16-step intervals in [2^20, 2^21)
+// (99.7 %; a miss costs an exact redo).  pll_pred_kernel and pll_sat_kernel leave these streams
+// to it when it is launched.
+constexpr float kPllPipeMin = 4194304.0f;     // 2^22
+constexpr float kPllPipeMin5 = 2097152.0f;    // 2^21
+constexpr float kPllPipeMinLow = 1048576.0f;  // 2^20
+__device__ inline bool pll_pipe_stream(float trig0, double step, float lo = kPllPipeMinLow,
                                        float hi = kPllTrigStick) {
     return trig0 >= lo && trig0 <= hi && trig0 == floorf(trig0) && fabs(step * (double)kPllTrigStick) < kPllMaxPr;
 }

@@ -119,6 +119,25 @@ __device__ inline float pick(float phase, float4 a, float ep) {
     return e;
 }
 
+// The same with five candidates: T = (T(c0 - 1), T(c0), T(c0 + 1), T(c0 + 2)), E = (e(c0 - 2) ..
+// e(c0 + 1)), e2 = e(c0 + 2).  Four compares into SGPR masks, then four v_cndmask, each reading a
+// mask written four VALU earlier (no wait state needed).
+__device__ inline float pick5(float phase, float4 T, float4 E, float e2) {
+    float e;
+    uint64_t m0, m1, m2, m3;
+    asm("v_cmp_ge_f32_e64 %1, %5, %6\n"
+        "v_cmp_ge_f32_e64 %2, %5, %7\n"
+        "v_cmp_ge_f32_e64 %3, %5, %8\n"
+        "v_cmp_ge_f32_e64 %4, %5, %9\n"
+        "v_cndmask_b32_e64 %0, %10, %11, %1\n"
+        "v_cndmask_b32_e64 %0, %0, %12, %2\n"
+        "v_cndmask_b32_e64 %0, %0, %13, %3\n"
+        "v_cndmask_b32_e64 %0, %0, %14, %4"
+        : "=&v"(e), "=&s"(m0), "=&s"(m1), "=&s"(m2), "=&s"(m3)
+        : "v"(phase), "v"(T.x), "v"(T.y), "v"(T.z), "v"(T.w), "v"(E.x), "v"(E.y), "v"(E.z), "v"(E.w), "v"(e2));
+    return e;
+}
+
 template <int NB>
 __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, int n_streams, int spw, size_t stride,
                                                       const double* side, size_t seg, double step, float norm_bw,
@@ -388,45 +407,50 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
 }
 
 
-// ---- pll_pipe_kernel: one stream a workgroup of three waves, trigOffset from 2^22 on ----------
+// ---- pll_pipe_kernel: one stream a workgroup of three waves, trigOffset from 2^20 on ----------
 //
 // pll_pred_kernel's chain wave issues ~16 VALU a step (the candidate choice, the updates, trigArg
-// and its check) and one wave issues a VALU per ~4 cycles, dependent or not
-// (tools/ubench_dep.hip, profiles/r03/ubench_dep.txt): its step costs its instruction count.  Here
-// the chain keeps only the recurrence -- the choice by two sign masks and bitfield inserts (no
-// VCC and its wait states), (Ki e, Kp e), the three float updates: ten VALU a step -- and hands
+// and its check), and one wave issues a VALU per ~4 cycles, dependent or not (tools/ubench_dep.hip,
+// profiles/r03/ubench_dep.txt): its step costs its instruction count.  Here the chain keeps only
+// the recurrence -- the candidate choice (compares of the phase into SGPR masks, v_cndmask), (Ki
+// e, Kp e), the three float updates: 8 VALU a step with NC = 3 candidates, 12 with 5 -- and hands
 // its phases to the other waves:
-//   wave 1: batch b + 2's e for the three candidates (lane (r, l): candidate c0 - 1 + r of step l);
-//   wave 2: rows 0-1 the phase thresholds of c0 and c0 + 1 ulp, c0's bits and P of batch b + 2;
-//           row 2 batch b - 1's trigArgs float(P + phase) (filter.cpp:165), their check against the
-//           candidates and the output stores.
-// Batch b + 2's candidates come from the phase at the start of batch b (tools/pll_predict.cpp
-// lookback 3), so the chain reads batch b + 1's data -- 20 16-byte reads at once -- right after
-// batch b's steps, where the reads overlap its phase stores and the barrier (spread over the
-// steps they stall it more: tools/ubench_chain.hip, profiles/r03/ubench_chain.txt).  A batch
-// whose trigArg missed its candidates -- E2 flags it in the interval after the chain ran it, the
-// chain reads the flag at the end of the next one -- is redone on the exact path with the two
-// after it (pll_redo from the recorded state); every wave takes two more barriers around that
-// redo, and the evaluators then redo batches b + 1 and b + 2 from the corrected phases.  From 2^22 the three
-// candidates held on every step of the bench stream (tools/pll_predict.cpp), so this is rare; the
-// output goes through pll_check_kernel like every runner's.
+//   wave 1: interval k + 1's e for the NC candidates c0 - NC/2 .. c0 + NC/2 of every step;
+//   wave 2: interval k + 1's NC - 1 phase thresholds a step, c0's bits and P; and interval
+//           k - 1's trigArgs float(P + phase) (filter.cpp:165) from the chain's phases, their
+//           check against the candidates and the output stores.
+// The candidates of interval k + 1 come from the phase at the start of interval k
+// (tools/pll_predict.cpp, lookback 2).  NC = 3 with 64-step intervals from 2^22 (every interval
+// of the bench stream hit), NC = 5 with 64-step intervals in [2^21, 2^22) (99.97 %) and with
+// 16-step ones in [2^20, 2^21) (99.7 %).  The chain reads an interval's data in bursts before
+// their steps (spread over the steps the reads stall it more: tools/ubench_chain.hip,
+// profiles/r03/ubench_chain.txt).  A missed interval -- wave 2 flags it in the interval after the
+// chain ran it, the chain reads the flag at the end of the next one -- is redone on the exact
+// path with the two after it (pll_redo from the recorded state); every wave takes two more
+// barriers around that redo, and the evaluators redo the next interval from the corrected
+// phase.  The output goes through pll_check_kernel like every runner's.
 
 // One wave a SIMD (amdgpu_waves_per_eu): the register budget is the chain's, so the scheduler
 // keeps each burst of reads whole instead of threading it through the steps for occupancy.
-template <int NB, int BPI, int RD>
+template <int NB, int BPI, int RD, int NC>
 __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))) pll_pipe_kernel(const float* io, int n, int n_streams, size_t stride,
                                                       const double* side, size_t seg, double step, float norm_bw,
                                                       const float* st, float* out_base, size_t ostride, int* fail,
                                                       float2* rec, size_t rb, int inject, int miss) {
     constexpr int NI = NB * BPI;
     static_assert(NI == 16 || NI == 32 || NI == 64, "the evaluators' lane map: 64 / NI lanes a step");
-    constexpr int LPS = 64 / NI;             // evaluator lanes a step
-    constexpr int CH = NI < 32 ? NI : 32;    // the chain's steps a burst of reads
-    // rings of four intervals (interval k in slot k & 3; interval 0 is batch 0): per step the
-    // thresholds T0, T1 and the e of c0 - 1 ulp and c0 (sel), the e of c0 + 1 ulp (sep),
-    // bits(c0) - 1 (scb), P (spr); the chain's phases (sph); per interval the check's verdict
-    // (smiss) and "redone exactly" (sexact)
+    static_assert(NC == 3 || NC == 5, "three or five candidates");
+    constexpr int LPS = 64 / NI;  // evaluator lanes a step
+    constexpr int HC = NC / 2;    // candidates c0 - HC .. c0 + HC
+    // the chain's steps a burst of reads (its registers hold a burst's data)
+    constexpr int CH = NC == 5 ? 16 : (NI < 32 ? NI : 32);
+    // rings of four intervals (interval k in slot k & 3; interval 0 is batch 0), per step: NC = 3:
+    // the thresholds of c0 and c0 + 1 ulp and the e of c0 - 1 and c0 (sel), the e of c0 + 1
+    // (sep); NC = 5: the thresholds of c0 - 1 .. c0 + 2 (sel), the e of c0 - 2 .. c0 + 1 (sel2),
+    // of c0 + 2 (sep); bits(c0) - HC (scb), P (spr); the chain's phases (sph); per interval the
+    // check's verdict (smiss) and "redone exactly" (sexact)
     __shared__ float4 sel[4][NI];
+    __shared__ float4 sel2[NC == 5 ? 4 : 1][NC == 5 ? NI : 1];
     __shared__ float sep[4][NI];
     __shared__ uint32_t scb[4][NI];
     __shared__ double spr[4][NI];
@@ -440,10 +464,11 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     const float Kp = norm_bw * static_cast<float>(2.666);
     const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
     PllState p{S[0], S[1], S[2], S[3], S[5]};
-    // the interval length's domain (uniform over the group): 64-step intervals from 2^22, 16-step
-    // ones in [2^21, 2^22)
-    if (!(NI == 64 ? pll_pipe_stream(p.trig, step, kPllPipeMin)
-                   : pll_pipe_stream(p.trig, step, kPllPipeMin16, kPllPipeMin - 1.0f)))
+    // the variant's domain (uniform over the group): NC = 3 from 2^22; NC = 5 with 64-step
+    // intervals in [2^21, 2^22), with 16-step ones in [2^20, 2^21)
+    if (!(NC == 3 ? pll_pipe_stream(p.trig, step, kPllPipeMin)
+                  : NI == 64 ? pll_pipe_stream(p.trig, step, kPllPipeMin5, kPllPipeMin - 1.0f)
+                             : pll_pipe_stream(p.trig, step, kPllPipeMinLow, kPllPipeMin5 - 1.0f)))
         return;
     const float trig0 = p.trig;
     const int nb = n / NB;
@@ -484,28 +509,25 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             pr = prs[j];
         };
         // interval k's candidate data from phase_ref, the phase at the start of interval k - 1:
-        // E1 lane (h, l) the e of candidates c0 - 1 + r of step l, r = h, h + LPS, ... < 3; E2
-        // lane (h, l) the thresholds of c0 + r, r = h, h + LPS, ... < 2, lanes h = 0 also c0's
-        // bits and P
+        // E1 lane (h, l) the e of candidates c0 - HC + r of step l, r = h, h + LPS, ... < NC; E2
+        // lane (h, l) the thresholds of c0 - HC + 1 + r, r = h, h + LPS, ... < NC - 1, lanes h = 0
+        // also c0's bits and P
         auto put = [&](int k, float phase_ref, float v, double iv, double pr) {
             const float c0 = (float)(pr + (double)phase_ref);
             const uint32_t cb = __builtin_bit_cast(uint32_t, c0);
             const int sl = k & 3;
             if (w == 1) {
-                for (int r = h; r < 3; r += LPS) {
-                    const float e = pred_e(__builtin_bit_cast(float, cb + (uint32_t)(r - 1)), v, iv);
-                    if (r == 0) sel[sl][l].z = e;
-                    else if (r == 1) sel[sl][l].w = e;
-                    else sep[sl][l] = e;
+                for (int r = h; r < NC; r += LPS) {
+                    const float e = pred_e(__builtin_bit_cast(float, cb + (uint32_t)(r - HC)), v, iv);
+                    if (r == NC - 1) sep[sl][l] = e;
+                    else if (NC == 3) reinterpret_cast<float*>(&sel[sl][l])[2 + r] = e;
+                    else reinterpret_cast<float*>(&sel2[NC == 5 ? sl : 0][NC == 5 ? l : 0])[r] = e;
                 }
             } else {
-                for (int r = h; r < 2; r += LPS) {
-                    const float T = phase_thr(pr, cb + (uint32_t)r);
-                    if (r == 0) sel[sl][l].x = T;
-                    else sel[sl][l].y = T;
-                }
+                for (int r = h; r < NC - 1; r += LPS)
+                    reinterpret_cast<float*>(&sel[sl][l])[r] = phase_thr(pr, cb + (uint32_t)(r + 1 - HC));
                 if (h == 0) {
-                    scb[sl][l] = cb - 1u;
+                    scb[sl][l] = cb - (uint32_t)HC;
                     spr[sl][l] = pr;
                 }
             }
@@ -524,9 +546,11 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             out[j0(k) + l] = a;
             const uint32_t cm = scb[sl][l];
             const float4 tt = sel[sl][l];
-            const float c0 = __builtin_bit_cast(float, cm + 1u);
-            const bool bad = (__builtin_bit_cast(uint32_t, a) - cm > 2u) || !(tt.x > -__builtin_inff()) ||
-                             !(tt.y > -__builtin_inff()) || !(c0 > 0.0f && c0 < 3.0e38f);
+            const float c0 = __builtin_bit_cast(float, cm + (uint32_t)HC);
+            const bool thr_ok = tt.x > -__builtin_inff() && tt.y > -__builtin_inff() &&
+                                (NC == 3 || (tt.z > -__builtin_inff() && tt.w > -__builtin_inff()));
+            const bool bad = (__builtin_bit_cast(uint32_t, a) - cm > (uint32_t)(NC - 1)) || !thr_ok ||
+                             !(c0 > 0.0f && c0 < 3.0e38f);
             bool any = __builtin_amdgcn_ballot_w64(bad) != 0;
             if (k == min(miss, ni)) any = true;  // test hook: a miss on interval `miss` (the redo path)
 #if defined(FMRX_AB_NOREAD) || defined(FMRX_AB_NOSTORE)
@@ -594,13 +618,14 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     exact(p, ctx, 0, 1);  // batch 0 on the exact path (see pll_spec_kernel)
     float integ = p.integ, phase = p.phase;
     // the carry: step 0's candidate data (those of the previous interval's last trigArg); after
-    // an exact stretch that trigArg's e itself in all three slots
-    float4 carry;
+    // an exact stretch that trigArg's e itself in every slot
+    float4 carry, carry2;
     float carry_ep;
     auto carry_exact = [&](float a, int k) {
         const int j = min(j0(k), n - 1);
         const float e = pred_e(a, x[j], ivs[j]);
-        carry = make_float4(0.0f, 0.0f, e, e);
+        carry = NC == 3 ? make_float4(0.0f, 0.0f, e, e) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        carry2 = make_float4(e, e, e, e);
         carry_ep = e;
     };
     carry_exact((float)ctx.x, 1);
@@ -619,10 +644,10 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         const int is = i & 3;
         const int flag = smiss[(i - 2) & 3];  // the verdict on interval i - 2 (slot 3 is clear at i = 1)
         const int kb = 1 + (i - 1) * BPI;         // the interval's first batch
-        // in bursts of CH steps: the data, 1.25 CH 16-byte reads at once in the order the steps
-        // need them (spread over the steps they stall the chain more, tools/ubench_chain.hip),
-        // then the steps, then their phases and batch records
-        float4 A[CH];
+        // in bursts of CH steps: the data, 1.25 CH (NC = 5: 2.25 CH) 16-byte reads at once in the
+        // order the steps need them (spread over the steps they stall the chain more,
+        // tools/ubench_chain.hip), then the steps, then their phases and batch records
+        float4 A[CH], A2[NC == 5 ? CH : 1];
         float EP[CH];
         unroll_ic(
             [&](auto hc) {
@@ -634,7 +659,10 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 for (int q = 0; q < CH / 4; q++) {
                     *reinterpret_cast<float4*>(&EP[4 * q]) = reinterpret_cast<const float4*>(&sep[is][H * CH])[q];
 #pragma unroll
-                    for (int u = 0; u < 4; u++) A[4 * q + u] = sel[is][H * CH + 4 * q + u];
+                    for (int u = 0; u < 4; u++) {
+                        A[4 * q + u] = sel[is][H * CH + 4 * q + u];
+                        if constexpr (NC == 5) A2[4 * q + u] = sel2[NC == 5 ? is : 0][NC == 5 ? H * CH + 4 * q + u : 0];
+                    }
                 }
                 float PH[CH];
                 float2 brec[CH / NB];  // (integ, phase) at the end of each batch of the burst
@@ -643,7 +671,11 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                         constexpr int J = decltype(jc)::value;
                         const float4 a = J == 0 ? carry : A[J > 0 ? J - 1 : 0];
                         const float ep = J == 0 ? carry_ep : EP[J > 0 ? J - 1 : 0];
-                        const float e = pick(phase, a, ep);
+                        float e;
+                        if constexpr (NC == 3)
+                            e = pick(phase, a, ep);
+                        else
+                            e = pick5(phase, a, J == 0 ? carry2 : A2[J > 0 ? J - 1 : 0], ep);
                         const float2v k = float2v{Ki, Kp} * e;
                         integ = integ + k.x;
                         phase = phase + (k.y + integ);
@@ -677,6 +709,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                     for (int q = 0; q < CH / NB; q++) rec[(size_t)s * rb + kb + H * (CH / NB) + q] = brec[q];
                 }
                 carry = A[CH - 1];
+                if constexpr (NC == 5) carry2 = A2[CH - 1];
                 carry_ep = EP[CH - 1];
             },
             std::make_integer_sequence<int, NI / CH>{});
@@ -770,15 +803,18 @@ void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_str
 
 void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_t stride, const double* side,
                      size_t seg, double step, float norm_bw, const float* st, float* out, size_t ostride, int* fail,
-                     float2* rec, size_t rb, int inject, int miss, bool long_iv, bool short_iv) {
+                     float2* rec, size_t rb, int inject, int miss, bool from22, bool from21, bool from20) {
 #ifdef FMRX_AB_PROF
     reg_pred_prof();
 #endif
-    if (long_iv)
-        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
+    if (from22)
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8, 3>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
                            stride, side, seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, miss);
-    if (short_iv)
-        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 1, 8>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
+    if (from21)
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
+                           stride, side, seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, miss);
+    if (from20)
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 1, 8, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
                            stride, side, seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, miss);
 }
 

@@ -958,10 +958,11 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         // (3 x streams <= SIMDs implies the two-wave runner fits too, so the lane kernel, told to
         // leave the predicted runners' streams, also leaves the three-wave runner's)
         const bool run_pipe = spec && pred_ok && pipe_env && spw == 1 && 3 * n_streams <= n_simd &&
-                              (!k || hi >= (double)kPllPipeMin16);
-        const bool pipe_all = run_pipe && k && lo >= (double)kPllPipeMin16;  // every stream to it
-        const bool pipe_long = run_pipe && (!k || hi >= (double)kPllPipeMin);
-        const bool pipe_short = run_pipe && (!k || lo < (double)kPllPipeMin);
+                              (!k || hi >= (double)kPllPipeMinLow);
+        const bool pipe_all = run_pipe && k && lo >= (double)kPllPipeMinLow;  // every stream to it
+        const bool pipe22 = run_pipe && (!k || hi >= (double)kPllPipeMin);
+        const bool pipe21 = run_pipe && (!k || (lo < (double)kPllPipeMin && hi >= (double)kPllPipeMin5));
+        const bool pipe20 = run_pipe && (!k || lo < (double)kPllPipeMin5);
         // the two-wave runner too wants a SIMD per wave (two of its waves on one SIMD ran slower
         // than the lane runner: 1,024 streams x 10 s 0.291 vs 0.279 s, 2,048 0.405 vs 0.371 s)
         const bool pred_fit = pred_ok && (2 * waves <= n_simd || pred_ok == 2);
@@ -993,10 +994,10 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
                 if (run_pred)
                     launch_pll_pred(waves, s, x, m, n_streams, spw, stride, side, seg, step, norm_bw, st, args, seg,
                                     fail, rec, rb, inject, run_sat ? 1 : 0, run_pipe ? 1 : 0);
-                // one stream a workgroup from trigOffset 2^21 (pll_pipe_stream)
+                // one stream a workgroup from trigOffset 2^20 (pll_pipe_stream)
                 if (run_pipe)
                     launch_pll_pipe(s, x, m, n_streams, stride, side, seg, step, norm_bw, st, args, seg, fail, rec,
-                                    rb, inject, pipe_miss, pipe_long, pipe_short);
+                                    rb, inject, pipe_miss, pipe22, pipe21, pipe20);
             } else
                 hipLaunchKernelGGL(pll_spec_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw,
                                    stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);

@@ -739,10 +739,10 @@ def test_pll_saturated_runner(fmrx, orc, monkeypatch, inject, sat, pipe, freq, n
 @pytest.mark.parametrize("pred,pipe", [("1", "1"), ("1", "0"), ("0", "0")])
 def test_pll_predicted_runner(fmrx, orc, monkeypatch, trig0, inject, pred, pipe):
     """Segments from trigOffset 2^20 up to the 2^24 stick: the predicted-trigArg runners
-    (pll_pred.hip: two waves from 2^20; three waves one stream a workgroup from 2^21, in 16-step
-    intervals below 2^22 and 64-step ones from there; FMRX_PLL_PIPE=0: the two-wave one
-    throughout; FMRX_PLL_PRED=0: the lane runner), starting at 2^20, at 2^21 + 33, 100 steps below
-    2^22 (the 16-step form runs on past it), at 2^22 + 17, and 5,000 steps below the stick (its pr
+    (pll_pred.hip: three waves one stream a workgroup -- five candidates in 16-step intervals from
+    2^20, in 64-step ones from 2^21, three candidates from 2^22; FMRX_PLL_PIPE=0: the two-wave
+    runner throughout; FMRX_PLL_PRED=0: the lane runner), starting at 2^20, at 2^21 + 33, 100 steps
+    below 2^22 (its form runs on past it), at 2^22 + 17, and 5,000 steps below the stick (its pr
     stops rising inside the segment); 2^20 - 1 stays on the lane runner.  A corrupted batch must
     be caught and resumed; without it every batch verifies."""
     monkeypatch.setenv("FMRX_PLL_PRED", pred)
@@ -771,15 +771,15 @@ def test_pll_predicted_runner(fmrx, orc, monkeypatch, trig0, inject, pred, pipe)
         assert (resumed > 0) if inject is not None else (resumed == 0), (resumed, checked)
 
 
-@pytest.mark.parametrize("trig0", [2097185.0, 4194321.0, 16772216.0, 16777216.0])
+@pytest.mark.parametrize("trig0", [1048600.0, 2097185.0, 4194321.0, 16772216.0, 16777216.0])
 @pytest.mark.parametrize("miss", ["1", "2", "150", "311", "312", "1248", "5000"])
 def test_pll_pipe_redo(fmrx, orc, monkeypatch, trig0, miss):
     """The three-wave runner's miss path (pll_pipe_kernel): FMRX_PLL_PIPE_MISS=k makes its check
     report interval k as missed (past the last interval: the last), so the chain redoes that
     interval and the two after it exactly and the evaluators restart from the corrected phase.
-    20,000 steps = batch 0 + 312 intervals of 64 steps + 1 batch from 2^22 (k = 1, 150, 311 and
+    20,000 steps = batch 0 + 312 intervals of 64 steps + 1 batch from 2^21 (k = 1, 150, 311 and
     312: the first, a middle one and the verdicts read after the loop), batch 0 + 1,249 intervals
-    of 16 steps below it (1,248 and 1,249 the last two).  Bit-exact, and every batch verifies."""
+    of 16 steps in [2^20, 2^21) (1,248 and 1,249 the last two).  Bit-exact, every batch verifies."""
     monkeypatch.setenv("FMRX_PLL_PIPE_MISS", miss)
     n = 20000
     rng = np.random.default_rng(int(trig0) % 977)
@@ -804,8 +804,8 @@ def test_pll_pipe_redo(fmrx, orc, monkeypatch, trig0, miss):
 
 def test_pipe_runner_streams(fmrx, monkeypatch):
     """pll_pipe_kernel over many streams (300: three waves each still fit the SIMDs), every
-    stream put at its own trigOffset through the state blob -- half of them in [2^22, 2^22 + 150)
-    (64-step intervals), half in [2^21, 2^21 + 150) (16-step intervals) -- 24 blocks in one call:
+    stream put at its own trigOffset through the state blob -- a third each from 2^22, 2^21 and
+    2^20 (the three forms) -- 24 blocks in one call:
     every batch verifies, and the PCM equals the same call with the three-wave runner off
     (FMRX_PLL_PIPE=0: the two-wave runner; both are checked by pll_check_kernel)."""
     ns, nb, bb = 300, 24, 12800
@@ -819,7 +819,7 @@ def test_pipe_runner_streams(fmrx, monkeypatch):
             hdr = np.frombuffer(bytes(blob[:40]), np.uint32)
             pll_off = 40 + ns * (int(hdr[6]) + 4 * int(hdr[7]) + 4 * 64)
             pll = np.frombuffer(bytes(blob[pll_off: pll_off + ns * 32]), np.float32).reshape(ns, 8).copy()
-            pll[:, 5] = np.where(np.arange(ns) % 2 == 0, 4194304.0, 2097152.0) + np.arange(ns) // 2
+            pll[:, 5] = np.array([4194304.0, 2097152.0, 1048576.0])[np.arange(ns) % 3] + np.arange(ns) // 3
             blob[pll_off: pll_off + ns * 32] = pll.tobytes()
             rx.set_state(bytes(blob))
             counts = torch.zeros(2, dtype=torch.int64, device="cuda")

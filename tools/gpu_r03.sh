@@ -3,7 +3,7 @@
 # the PLL runner tests, the three-wave runner's cycles per interval (A/B build with FMRX_AB_PROF)
 # and configs[2].
 set -o pipefail
-OUT=gpurun_out/r03_pipe21
+OUT=gpurun_out/r03_pipe22
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -k "predicted or saturated or speculation or pipe or long_hash or bench_config or trig_hint or many_streams" -x -q --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }

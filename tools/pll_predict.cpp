@@ -76,17 +76,17 @@ int main(int argc, char** argv) {
         pmax = std::fmax(pmax, phase[i]);
     }
     std::printf("phase range [%g, %g]\n", pmin, pmax);
-    std::printf("%-22s %5s %9s %9s %9s %9s %12s\n", "j range", "B", "k=0", "|k|<=1", "|k|<=2", "|k|>2",
-                "batch|k|<=1");
+    std::printf("%-22s %5s %9s %9s %9s %9s %12s %12s\n", "j range", "B", "k=0", "|k|<=1", "|k|<=2", "|k|>2",
+                "batch|k|<=1", "batch|k|<=2");
     for (int r = 0; r + 1 < 8; r++) {
         const size_t j0 = edges[r], j1 = std::min(edges[r + 1], N);
         if (j0 >= j1) continue;
         for (int B : batches) {
-            long k0 = 0, k1 = 0, k2 = 0, kx = 0, nb_all = 0, nb_ok = 0;
+            long k0 = 0, k1 = 0, k2 = 0, kx = 0, nb_all = 0, nb_ok = 0, nb_ok2 = 0;
             for (size_t b0 = (j0 / B) * B; b0 < j1; b0 += B) {
                 const size_t back = (size_t)(lb - 1) * B + 1;  // the last step of batch b - lb
                 const float p0 = b0 >= back ? phase[b0 - back] : 0.0f;
-                bool ok = true;
+                bool ok = true, ok2 = true;
                 for (size_t j = b0; j < b0 + B && j < j1; j++) {
                     if (j < j0) continue;
                     const float cand = (float)(w * (double)std::min((float)(j + 1), 16777216.0f) + (double)p0);
@@ -96,14 +96,16 @@ int main(int argc, char** argv) {
                     if (k <= 2) k2++;
                     else kx++;
                     ok = ok && k <= 1;
+                    ok2 = ok2 && k <= 2;
                 }
                 nb_all++;
                 nb_ok += ok;
+                nb_ok2 += ok2;
             }
             const double tot = (double)(j1 - j0);
-            std::printf("[2^%-4.1f, 2^%-4.1f)     %5d %9.4f %9.4f %9.4f %9.4f %12.4f\n", j0 ? std::log2((double)j0) : 0.0,
-                        std::log2((double)j1), B, k0 / tot, k1 / tot, k2 / tot, kx / tot,
-                        (double)nb_ok / nb_all);
+            std::printf("[2^%-4.1f, 2^%-4.1f)     %5d %9.4f %9.4f %9.4f %9.4f %12.4f %12.4f\n",
+                        j0 ? std::log2((double)j0) : 0.0, std::log2((double)j1), B, k0 / tot, k1 / tot, k2 / tot,
+                        kx / tot, (double)nb_ok / nb_all, (double)nb_ok2 / nb_all);
         }
     }
     // two candidates: c0 and its neighbour on the side of the exact sum P + phase_ref (the
