@@ -138,6 +138,76 @@ __device__ inline float pick5(float phase, float4 T, float4 E, float e2) {
     return e;
 }
 
+// Four of pll_pipe_kernel's chain steps in one asm block: per step the candidate choice (pick /
+// pick5), (Ki e, Kp e) as one v_pk_mul_f32 with (Ki, Kp) in an SGPR pair (kk: Ki low, Kp high),
+// and the three float updates integ += Ki e, phase += Kp e + integ (filter.cpp:161-162), each
+// product and sum rounded on its own as there.  9 instructions a step with three candidates, 12
+// with five.  Compiled step by step, the same chain issued 11 and 14: the compiler puts a wait
+// state after every asm statement whose result a VALU reads (it cannot see the statement's last
+// instruction), and another after a v_pk_mul_f32 reading (Ki, Kp) from VGPRs; here one wait
+// state follows each block of four (tools/ubench_chain.hip modes 9 and 20).  e and the two
+// products live in v252-v255, clobbered.  ph[k] = the phase after step k.
+#define FMRX_CHAIN_TAIL(P, Q)                                    \
+    "v_pk_mul_f32 v[254:255], v[252:253], %[kk] op_sel_hi:[0,1]\n" \
+    "v_add_f32 %[ig], %[ig], v254\n"                             \
+    "v_add_f32 v255, v255, %[ig]\n"                              \
+    "v_add_f32 " Q ", " P ", v255\n"
+#define FMRX_CHAIN_STEP3(P, Q, K)                                      \
+    "v_cmp_ge_f32_e64 %[m0], " P ", %[ta" #K "]\n"                       \
+    "v_cmp_ge_f32_e64 %[m1], " P ", %[tb" #K "]\n"                       \
+    "s_nop 0\n"                                                        \
+    "v_cndmask_b32_e64 v252, %[ea" #K "], %[eb" #K "], %[m0]\n"          \
+    "v_cndmask_b32_e64 v252, v252, %[ec" #K "], %[m1]\n" FMRX_CHAIN_TAIL(P, Q)
+#define FMRX_CHAIN_STEP5(P, Q, K)                                      \
+    "v_cmp_ge_f32_e64 %[m0], " P ", %[ta" #K "]\n"                       \
+    "v_cmp_ge_f32_e64 %[m1], " P ", %[tb" #K "]\n"                       \
+    "v_cmp_ge_f32_e64 %[m2], " P ", %[tc" #K "]\n"                       \
+    "v_cmp_ge_f32_e64 %[m3], " P ", %[td" #K "]\n"                       \
+    "v_cndmask_b32_e64 v252, %[ea" #K "], %[eb" #K "], %[m0]\n"          \
+    "v_cndmask_b32_e64 v252, v252, %[ec" #K "], %[m1]\n"                 \
+    "v_cndmask_b32_e64 v252, v252, %[ed" #K "], %[m2]\n"                 \
+    "v_cndmask_b32_e64 v252, v252, %[ee" #K "], %[m3]\n" FMRX_CHAIN_TAIL(P, Q)
+#define FMRX_CHAIN_OUTS \
+    [q0] "=&v"(ph[0]), [q1] "=&v"(ph[1]), [q2] "=&v"(ph[2]), [q3] "=&v"(ph[3]), [ig] "+v"(integ)
+
+// a[k] = (T0, T1, e(c0 - 1), e(c0)), ep[k] = e(c0 + 1) of step k (pick's arguments)
+__device__ inline void chain4_3(float phase, float& integ, uint64_t kk, const float4 (&a)[4], const float (&ep)[4],
+                                float (&ph)[4]) {
+    uint64_t m0, m1;
+    asm volatile(FMRX_CHAIN_STEP3("%[p]", "%[q0]", 0) FMRX_CHAIN_STEP3("%[q0]", "%[q1]", 1)
+                     FMRX_CHAIN_STEP3("%[q1]", "%[q2]", 2) FMRX_CHAIN_STEP3("%[q2]", "%[q3]", 3)
+                 : FMRX_CHAIN_OUTS, [m0] "=&s"(m0), [m1] "=&s"(m1)
+                 : [p] "v"(phase), [kk] "s"(kk),
+                   [ta0] "v"(a[0].x), [tb0] "v"(a[0].y), [ea0] "v"(a[0].z), [eb0] "v"(a[0].w), [ec0] "v"(ep[0]),
+                   [ta1] "v"(a[1].x), [tb1] "v"(a[1].y), [ea1] "v"(a[1].z), [eb1] "v"(a[1].w), [ec1] "v"(ep[1]),
+                   [ta2] "v"(a[2].x), [tb2] "v"(a[2].y), [ea2] "v"(a[2].z), [eb2] "v"(a[2].w), [ec2] "v"(ep[2]),
+                   [ta3] "v"(a[3].x), [tb3] "v"(a[3].y), [ea3] "v"(a[3].z), [eb3] "v"(a[3].w), [ec3] "v"(ep[3])
+                 : "v252", "v253", "v254", "v255");
+}
+
+// T[k], E[k], e2[k]: pick5's arguments of step k
+__device__ inline void chain4_5(float phase, float& integ, uint64_t kk, const float4 (&T)[4], const float4 (&E)[4],
+                                const float (&e2)[4], float (&ph)[4]) {
+    uint64_t m0, m1, m2, m3;
+    asm volatile(FMRX_CHAIN_STEP5("%[p]", "%[q0]", 0) FMRX_CHAIN_STEP5("%[q0]", "%[q1]", 1)
+                     FMRX_CHAIN_STEP5("%[q1]", "%[q2]", 2) FMRX_CHAIN_STEP5("%[q2]", "%[q3]", 3)
+                 : FMRX_CHAIN_OUTS, [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3)
+                 : [p] "v"(phase), [kk] "s"(kk),
+                   [ta0] "v"(T[0].x), [tb0] "v"(T[0].y), [tc0] "v"(T[0].z), [td0] "v"(T[0].w),
+                   [ea0] "v"(E[0].x), [eb0] "v"(E[0].y), [ec0] "v"(E[0].z), [ed0] "v"(E[0].w), [ee0] "v"(e2[0]),
+                   [ta1] "v"(T[1].x), [tb1] "v"(T[1].y), [tc1] "v"(T[1].z), [td1] "v"(T[1].w),
+                   [ea1] "v"(E[1].x), [eb1] "v"(E[1].y), [ec1] "v"(E[1].z), [ed1] "v"(E[1].w), [ee1] "v"(e2[1]),
+                   [ta2] "v"(T[2].x), [tb2] "v"(T[2].y), [tc2] "v"(T[2].z), [td2] "v"(T[2].w),
+                   [ea2] "v"(E[2].x), [eb2] "v"(E[2].y), [ec2] "v"(E[2].z), [ed2] "v"(E[2].w), [ee2] "v"(e2[2]),
+                   [ta3] "v"(T[3].x), [tb3] "v"(T[3].y), [tc3] "v"(T[3].z), [td3] "v"(T[3].w),
+                   [ea3] "v"(E[3].x), [eb3] "v"(E[3].y), [ec3] "v"(E[3].z), [ed3] "v"(E[3].w), [ee3] "v"(e2[3])
+                 : "v252", "v253", "v254", "v255");
+}
+#undef FMRX_CHAIN_OUTS
+#undef FMRX_CHAIN_STEP5
+#undef FMRX_CHAIN_STEP3
+#undef FMRX_CHAIN_TAIL
+
 template <int NB>
 __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, int n_streams, int spw, size_t stride,
                                                       const double* side, size_t seg, double step, float norm_bw,
@@ -456,6 +526,9 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     __shared__ double spr[4][NI];
     __shared__ float sph[4][NI];
     __shared__ int smiss[4], sexact[4];
+#ifdef FMRX_AB_STOREALL
+    __shared__ float4 sdum[64 + NI / 4];
+#endif
     const int w = threadIdx.x >> 6, t = threadIdx.x & 63, l = t & (NI - 1), h = t / NI;
     const int s = blockIdx.x;  // grid = n_streams
     const float* x = io + (size_t)s * stride;
@@ -617,6 +690,9 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     ctx.valid = false;
     exact(p, ctx, 0, 1);  // batch 0 on the exact path (see pll_spec_kernel)
     float integ = p.integ, phase = p.phase;
+    // (Ki, Kp) as an SGPR pair for the chain's v_pk_mul_f32 (uniform: readfirstlane)
+    const uint64_t kk = (uint64_t)__builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, Ki)) |
+                        ((uint64_t)__builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, Kp)) << 32);
     // the carry: step 0's candidate data (those of the previous interval's last trigArg); after
     // an exact stretch that trigArg's e itself in every slot
     float4 carry, carry2;
@@ -667,22 +743,27 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 float PH[CH];
                 float2 brec[CH / NB];  // (integ, phase) at the end of each batch of the burst
                 unroll_ic(
-                    [&](auto jc) {
-                        constexpr int J = decltype(jc)::value;
-                        const float4 a = J == 0 ? carry : A[J > 0 ? J - 1 : 0];
-                        const float ep = J == 0 ? carry_ep : EP[J > 0 ? J - 1 : 0];
-                        float e;
+                    [&](auto gc) {
+                        constexpr int J = 4 * decltype(gc)::value;  // steps J .. J + 3
+                        float4 a[4], a2[4];
+                        float ep[4];
+#pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            a[u] = J + u == 0 ? carry : A[J + u > 0 ? J + u - 1 : 0];
+                            ep[u] = J + u == 0 ? carry_ep : EP[J + u > 0 ? J + u - 1 : 0];
+                            if constexpr (NC == 5) a2[u] = J + u == 0 ? carry2 : A2[J + u > 0 ? J + u - 1 : 0];
+                        }
+                        float q[4];
                         if constexpr (NC == 3)
-                            e = pick(phase, a, ep);
+                            chain4_3(phase, integ, kk, a, ep, q);
                         else
-                            e = pick5(phase, a, J == 0 ? carry2 : A2[J > 0 ? J - 1 : 0], ep);
-                        const float2v k = float2v{Ki, Kp} * e;
-                        integ = integ + k.x;
-                        phase = phase + (k.y + integ);
-                        PH[J] = phase;
-                        if constexpr (J % NB == NB - 1) brec[J / NB] = make_float2(integ, phase);
+                            chain4_5(phase, integ, kk, a, a2, ep, q);
+#pragma unroll
+                        for (int u = 0; u < 4; u++) PH[J + u] = q[u];
+                        phase = q[3];
+                        if constexpr ((J + 3) % NB == NB - 1) brec[(J + 3) / NB] = make_float2(integ, phase);
                     },
-                    std::make_integer_sequence<int, CH>{});
+                    std::make_integer_sequence<int, CH / 4>{});
                 if constexpr (H == NI / CH - 1) {
                     if (inj >= kb && inj < kb + BPI) {  // test hook, at the interval's end
                         phase += 1.0e-3f;
@@ -697,6 +778,17 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 __builtin_amdgcn_sched_barrier(0);
                 __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
                 __builtin_amdgcn_sched_barrier(0);
+#ifdef FMRX_AB_STOREALL  // A/B: the phase stores from every lane, lanes 1-63 to a scratch row
+                {
+                    float4* wp = t == 0 ? reinterpret_cast<float4*>(&sph[is][H * CH]) : &sdum[t];
+#pragma unroll
+                    for (int q = 0; q < CH / 4; q++) wp[q] = *reinterpret_cast<const float4*>(&PH[4 * q]);
+                }
+                if (t == 0) {
+#pragma unroll
+                    for (int q = 0; q < CH / NB; q++) rec[(size_t)s * rb + kb + H * (CH / NB) + q] = brec[q];
+                }
+#else
 #ifdef FMRX_AB_NOSTORE  // A/B timing only (wrong results): no phase or record stores
                 if (t == 0 && phase == 12345.0f) {
 #else
@@ -708,6 +800,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
                     for (int q = 0; q < CH / NB; q++) rec[(size_t)s * rb + kb + H * (CH / NB) + q] = brec[q];
                 }
+#endif
                 carry = A[CH - 1];
                 if constexpr (NC == 5) carry2 = A2[CH - 1];
                 carry_ep = EP[CH - 1];

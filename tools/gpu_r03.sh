@@ -1,15 +1,15 @@
 #!/bin/bash
 # tools/gpu_r03.sh — the current round-3 GPU check (edited per run; one recipe, not one per run):
-# the whole GPU suite, smoke(), the default bench line and the stereo stream-count sweep.
+# the PLL runner tests with the four-step chain blocks, configs[2] with them, and configs[2]
+# with the branch-free phase stores (A/B build, FMRX_AB_STOREALL).
 set -o pipefail
-OUT=gpurun_out/r03_full3
+OUT=gpurun_out/r03_blk4
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
-tail -2 $OUT/tests.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || { tail $OUT/smoke.log; exit 2; }
-tail -1 $OUT/smoke.log
-timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 3; }
-cat $OUT/bench.json
-timeout -k 10 400 python tools/bench_stereo.py --streams 1 32 256 1024 2048 > $OUT/streams.json 2>&1 || { tail $OUT/streams.json; exit 4; }
-grep -v amdgpu.ids $OUT/streams.json
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -k "predicted or saturated or speculation or pipe or long_hash or bench_config or trig_hint or many_streams" -x -q --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
+timeout -k 10 300 python tools/bench_stereo.py --gib > $OUT/gib.json 2>&1 || { tail $OUT/gib.json; exit 2; }
+grep -v amdgpu.ids $OUT/gib.json
+AB=software-defined-radio-course-project_amd/build_ab/libfmrx.so
+FMRX_LIB_PATH=$AB timeout -k 10 300 python tools/bench_stereo.py --gib > $OUT/gib_ab.json 2>&1 || { tail $OUT/gib_ab.json; exit 3; }
+grep -v amdgpu.ids $OUT/gib_ab.json

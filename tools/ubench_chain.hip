@@ -17,6 +17,20 @@
 //   mode 12: mode 9 + the phases stored to LDS after the batch from lane 0 (exec-masked branch),
 //   mode 13: mode 9 + each group of 4 phases stored as soon as made, every lane to one address,
 //   mode 14: mode 9 + each group of 4 phases stored as soon as made, lane 0 only (exec in asm),
+//   mode 15: mode 9 with the choice in C (ternaries; the compiler places the wait states),
+//   mode 16: mode 15 + the next batch's data read during the steps, one read placed by
+//            sched_group_barrier in each wait-state slot (between the compares and the selects,
+//            and before the multiply),
+//   mode 17: mode 9 with (Ki e, Kp e) as two v_mul_f32 instead of v_pk_mul_f32,
+//   mode 18: mode 9 with the next batch's 16-B reads inside the choice's asm block in place of
+//            its s_nop (timing only: the compiler does not know those registers are in flight),
+//   mode 19: mode 17 + mode 2's reads (one a step, compiler-placed),
+//   mode 20: the whole step in one asm block with fresh outputs (compares, s_nop, selects, two
+//            v_mul_f32, three adds: 10 instructions, no copies),
+//   mode 21: mode 20 with the next batch's 16-B read in the s_nop's place, its ep reads every
+//            fourth step and the phases stored to LDS four at a time (lane 0 to the ring, the
+//            other lanes to a scratch row: no exec mask, no branch),
+//   mode 22: mode 21 with EXEC = lane 0 over the batch's steps (set and restored in asm),
 // and the other waves (0, 1 or 2 of them) either idle at the barrier or busy with f64 FMAs
 // (`busy`); one barrier per batch when there are other waves.  Prints shader cycles per step.
 //
@@ -71,6 +85,7 @@ __global__ void __launch_bounds__(192) chain(float* out, long long* cyc, int nb,
     __shared__ float4 sel[2][NB];
     __shared__ float sep[2][NB];
     __shared__ float4 sph[2][NB / 4];
+    __shared__ float4 sdum[64 + NB / 2];
     const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
     const int nw = blockDim.x >> 6;
     if (threadIdx.x < 2 * NB) {
@@ -128,6 +143,8 @@ __global__ void __launch_bounds__(192) chain(float* out, long long* cyc, int nb,
             for (int J = 0; J < NB / 4; J++)
                 *reinterpret_cast<float4*>(&EP[4 * J]) = reinterpret_cast<const float4*>(sep[b & 1])[J];
         }
+        if constexpr (MODE == 18 || MODE >= 21) __builtin_amdgcn_s_waitcnt(0xC07F);  // the asm's reads (previous batch)
+        if constexpr (MODE == 22) asm volatile("s_mov_b64 s[44:45], exec\n s_mov_b64 exec, 1" ::: "s44", "s45");
         float PH[NB] = {};
         if (MODE != 3 || t < 16)  // mode 3: lanes 16-63 sit out
         unroll_ic(
@@ -138,8 +155,14 @@ __global__ void __launch_bounds__(192) chain(float* out, long long* cyc, int nb,
                     if constexpr (J % 4 == 0)
                         *reinterpret_cast<float4*>(&NEP[J]) = reinterpret_cast<const float4*>(sep[(b + 1) & 1])[J / 4];
                 }
-                const float4 a = (MODE == 0 || MODE == 6 || MODE >= 9) ? A0[J] : A[J];
-                const float ep = (MODE == 0 || MODE == 6 || MODE >= 9) ? E0[J] : EP[J];
+                if constexpr (MODE == 19) {
+                    NA[J] = sel[(b + 1) & 1][J];
+                    if constexpr (J % 4 == 0)
+                        *reinterpret_cast<float4*>(&NEP[J]) = reinterpret_cast<const float4*>(sep[(b + 1) & 1])[J / 4];
+                }
+                const bool regs = MODE == 0 || MODE == 6 || (MODE >= 9 && MODE != 16 && MODE != 18 && MODE != 19 && MODE != 21 && MODE != 22);
+                const float4 a = regs ? A0[J] : A[J];
+                const float ep = regs ? E0[J] : EP[J];
                 (void)0;
                 float e;
                 if constexpr (MODE == 10 || MODE == 11) {
@@ -164,6 +187,72 @@ __global__ void __launch_bounds__(192) chain(float* out, long long* cyc, int nb,
                             : "s40", "s41", "s42", "s43");
                     PH[J] = phase;
                     (void)e;
+                } else if constexpr (MODE == 15 || MODE == 16) {
+                    if constexpr (MODE == 16) {
+                        NA[J] = sel[(b + 1) & 1][J];
+                        if constexpr (J % 4 == 0)
+                            *reinterpret_cast<float4*>(&NEP[J]) = reinterpret_cast<const float4*>(sep[(b + 1) & 1])[J / 4];
+                    }
+                    const bool m0 = phase >= a.x, m1 = phase >= a.y;
+                    e = m1 ? ep : (m0 ? a.w : a.z);
+                } else if constexpr (MODE == 18) {
+                    const unsigned na = (unsigned)(uintptr_t)&sel[(b + 1) & 1][J];
+                    f4 v;
+                    asm volatile(
+                        "v_cmp_ge_f32_e64 s[40:41], %2, %3\n v_cmp_ge_f32_e64 s[42:43], %2, %4\n ds_read_b128 %1, %8\n"
+                        " v_cndmask_b32_e64 %0, %5, %6, s[40:41]\n v_cndmask_b32_e64 %0, %0, %7, s[42:43]"
+                        : "=&v"(e), "=&v"(v)
+                        : "v"(phase), "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(ep), "v"(na)
+                        : "s40", "s41", "s42", "s43");
+                    NA[J] = make_float4(v.x, v.y, v.z, v.w);
+                    if constexpr (J % 4 == 0)
+                        *reinterpret_cast<float4*>(&NEP[J]) = reinterpret_cast<const float4*>(sep[(b + 1) & 1])[J / 4];
+                } else if constexpr (MODE == 20 || MODE == 21 || MODE == 22) {
+                    float e, ka, kb, ig, ph;
+                    uint64_t m0, m1;
+                    f4 nx;
+                    if constexpr (MODE == 20)
+                        asm volatile(
+                            "v_cmp_ge_f32_e64 %[m0], %[p], %[t0]\n v_cmp_ge_f32_e64 %[m1], %[p], %[t1]\n s_nop 0\n"
+                            " v_cndmask_b32_e64 %[e], %[em], %[e0], %[m0]\n v_cndmask_b32_e64 %[e], %[e], %[ep], %[m1]\n"
+                            " v_mul_f32 %[ka], %[ki], %[e]\n v_mul_f32 %[kb], %[kp], %[e]\n"
+                            " v_add_f32 %[ig], %[ii], %[ka]\n v_add_f32 %[kb], %[kb], %[ig]\n v_add_f32 %[ph], %[p], %[kb]"
+                            : [e] "=&v"(e), [ka] "=&v"(ka), [kb] "=&v"(kb), [ig] "=&v"(ig), [ph] "=&v"(ph),
+                              [m0] "=&s"(m0), [m1] "=&s"(m1)
+                            : [p] "v"(phase), [ii] "v"(integ), [t0] "v"(a.x), [t1] "v"(a.y), [em] "v"(a.z),
+                              [e0] "v"(a.w), [ep] "v"(ep), [ki] "v"(Ki), [kp] "v"(Kp));
+                    else
+                        asm volatile(
+                            "v_cmp_ge_f32_e64 %[m0], %[p], %[t0]\n v_cmp_ge_f32_e64 %[m1], %[p], %[t1]\n"
+                            " ds_read_b128 %[nx], %[ra] offset:%[ro]\n"
+                            " v_cndmask_b32_e64 %[e], %[em], %[e0], %[m0]\n v_cndmask_b32_e64 %[e], %[e], %[ep], %[m1]\n"
+                            " v_mul_f32 %[ka], %[ki], %[e]\n v_mul_f32 %[kb], %[kp], %[e]\n"
+                            " v_add_f32 %[ig], %[ii], %[ka]\n v_add_f32 %[kb], %[kb], %[ig]\n v_add_f32 %[ph], %[p], %[kb]"
+                            : [e] "=&v"(e), [ka] "=&v"(ka), [kb] "=&v"(kb), [ig] "=&v"(ig), [ph] "=&v"(ph),
+                              [m0] "=&s"(m0), [m1] "=&s"(m1), [nx] "=&v"(nx)
+                            : [p] "v"(phase), [ii] "v"(integ), [t0] "v"(a.x), [t1] "v"(a.y), [em] "v"(a.z),
+                              [e0] "v"(a.w), [ep] "v"(ep), [ki] "v"(Ki), [kp] "v"(Kp),
+                              [ra] "v"((unsigned)(uintptr_t)&sel[(b + 1) & 1][0]), [ro] "i"(16 * J));
+                    if constexpr (MODE >= 21) {
+                        NA[J] = make_float4(nx.x, nx.y, nx.z, nx.w);
+                        if constexpr (J % 4 == 0) {
+                            f4 ne;
+                            asm volatile("ds_read_b128 %0, %1 offset:%2"
+                                         : "=v"(ne) : "v"((unsigned)(uintptr_t)&sep[(b + 1) & 1][0]), "i"(4 * J));
+                            NEP[J] = ne.x; NEP[J + 1] = ne.y; NEP[J + 2] = ne.z; NEP[J + 3] = ne.w;
+                        }
+                    }
+                    integ = ig;
+                    phase = ph;
+                    PH[J] = phase;
+                    e = 0.0f;
+                    (void)e;
+                    if constexpr (MODE >= 21 && J % 4 == 3) {
+                        const unsigned wa = t == 0 ? (unsigned)(uintptr_t)&sph[b & 1][0]
+                                                   : (unsigned)(uintptr_t)&sdum[t];
+                        const f4 v = {PH[J - 3], PH[J - 2], PH[J - 1], PH[J]};
+                        asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(wa), "v"(v), "i"(4 * (J - 3)) : "memory");
+                    }
                 } else if constexpr (MODE == 9 || MODE >= 12) {
                     asm volatile(
                         "v_cmp_ge_f32_e64 s[40:41], %1, %2\n v_cmp_ge_f32_e64 s[42:43], %1, %3\n s_nop 0\n"
@@ -181,7 +270,14 @@ __global__ void __launch_bounds__(192) chain(float* out, long long* cyc, int nb,
                     const uint32_t m0 = sign_mask(phase - a.x), m1 = sign_mask(phase - a.y);
                     e = bfi(m1, bfi(m0, a.z, a.w), ep);
                 }
-                if constexpr (MODE != 10 && MODE != 11) {
+                if constexpr (MODE == 17 || MODE == 19) {
+                    float k1 = Ki * e;
+                    asm("" : "+v"(k1));  // keeps the two products apart (no v_pk_mul_f32)
+                    const float k2 = Kp * e;
+                    integ = integ + k1;
+                    phase = phase + (k2 + integ);
+                    PH[J] = phase;
+                } else if constexpr (MODE != 10 && MODE != 11 && MODE != 20 && MODE != 21 && MODE != 22) {
                     const float2v k = float2v{Ki, Kp} * e;
                     integ = integ + k.x;
                     phase = phase + (k.y + integ);
@@ -198,9 +294,19 @@ __global__ void __launch_bounds__(192) chain(float* out, long long* cyc, int nb,
                                      " s_mov_b64 exec, s[44:45]" ::"v"(a), "v"(v) : "s44", "s45", "memory");
                     }
                 }
-                if constexpr (MODE == 2 || MODE == 3) __builtin_amdgcn_sched_barrier(0);
+                if constexpr (MODE == 16) {
+                    // cmp, cmp | read | cndmask, cndmask | read (every 4th step) | pk_mul | adds
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, J);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, J);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, J);
+                    if constexpr (J % 4 == 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, J);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 4, J);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if constexpr (MODE == 2 || MODE == 3 || MODE == 18 || MODE == 19) __builtin_amdgcn_sched_barrier(0);
             },
             std::make_integer_sequence<int, NB>{});
+        if constexpr (MODE == 22) asm volatile("s_mov_b64 exec, s[44:45]" ::: "memory");
         if constexpr (MODE == 12) {
             if (t == 0) {
 #pragma unroll
@@ -264,6 +370,14 @@ int main() {
             run<12>(waves, busy, d_out, d_cyc);
             run<13>(waves, busy, d_out, d_cyc);
             run<14>(waves, busy, d_out, d_cyc);
+            run<15>(waves, busy, d_out, d_cyc);
+            run<16>(waves, busy, d_out, d_cyc);
+            run<17>(waves, busy, d_out, d_cyc);
+            run<18>(waves, busy, d_out, d_cyc);
+            run<19>(waves, busy, d_out, d_cyc);
+            run<20>(waves, busy, d_out, d_cyc);
+            run<21>(waves, busy, d_out, d_cyc);
+            run<22>(waves, busy, d_out, d_cyc);
         }
     }
     (void)hipFree(d_out);
