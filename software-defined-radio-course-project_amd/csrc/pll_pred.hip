@@ -481,14 +481,16 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
 //
 // pll_pred_kernel's chain wave issues ~16 VALU a step (the candidate choice, the updates, trigArg
 // and its check), and one wave issues a VALU per ~4 cycles, dependent or not (tools/ubench_dep.hip,
-// profiles/r03/ubench_dep.txt): its step costs its instruction count.  Here the chain keeps only
-// the recurrence -- the candidate choice (compares of the phase into SGPR masks, v_cndmask), (Ki
-// e, Kp e), the three float updates: 8 VALU a step with NC = 3 candidates, 12 with 5 -- and hands
-// its phases to the other waves:
+// profiles/r03/ubench_dep.txt): its step costs its instruction count, wait states included.  Here
+// the chain keeps only the recurrence -- the candidate choice (compares of the phase into SGPR
+// masks, v_cndmask), (Ki e, Kp e), the three float updates: 9 instructions a step with NC = 3
+// candidates, 12 with 5, four steps an asm block (chain4_3 / chain4_5) -- and hands one state a
+// batch, (integ, phase) after its last step, to the other waves:
 //   wave 1: interval k + 1's e for the NC candidates c0 - NC/2 .. c0 + NC/2 of every step;
 //   wave 2: interval k + 1's NC - 1 phase thresholds a step, c0's bits and P; and interval
-//           k - 1's trigArgs float(P + phase) (filter.cpp:165) from the chain's phases, their
-//           check against the candidates and the output stores.
+//           k - 1 replayed batch by batch from those states, one lane group a batch (the chain's
+//           arithmetic on the same data, so the same phases), its trigArgs float(P + phase)
+//           (filter.cpp:165), their check against the candidates and the output stores.
 // The candidates of interval k + 1 come from the phase at the start of interval k
 // (tools/pll_predict.cpp, lookback 2).  NC = 3 with 64-step intervals from 2^22 (every interval
 // of the bench stream hit), NC = 5 with 64-step intervals in [2^21, 2^22) (99.97 %) and with
@@ -513,30 +515,35 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     constexpr int LPS = 64 / NI;  // evaluator lanes a step
     constexpr int HC = NC / 2;    // candidates c0 - HC .. c0 + HC
     // the chain's steps a burst of reads (its registers hold a burst's data)
-    constexpr int CH = NC == 5 ? 16 : (NI < 32 ? NI : 32);
+#ifndef FMRX_CHM
+#define FMRX_CHM 32
+#endif
+    constexpr int CHM = FMRX_CHM;
+    constexpr int CH = NC == 5 ? 16 : (NI < CHM ? NI : CHM);
     // rings of four intervals (interval k in slot k & 3; interval 0 is batch 0), per step: NC = 3:
     // the thresholds of c0 and c0 + 1 ulp and the e of c0 - 1 and c0 (sel), the e of c0 + 1
     // (sep); NC = 5: the thresholds of c0 - 1 .. c0 + 2 (sel), the e of c0 - 2 .. c0 + 1 (sel2),
-    // of c0 + 2 (sep); bits(c0) - HC (scb), P (spr); the chain's phases (sph); per interval the
-    // check's verdict (smiss) and "redone exactly" (sexact)
+    // of c0 + 2 (sep); bits(c0) - HC (scb), P (spr); the chain's (integ, phase) at the end of each
+    // batch (sst); per interval the check's verdict (smiss) and "redone exactly" (sexact)
     __shared__ float4 sel[4][NI];
     __shared__ float4 sel2[NC == 5 ? 4 : 1][NC == 5 ? NI : 1];
     __shared__ float sep[4][NI];
     __shared__ uint32_t scb[4][NI];
     __shared__ double spr[4][NI];
-    __shared__ float sph[4][NI];
+    __shared__ float2 sst[4][BPI];
     __shared__ int smiss[4], sexact[4];
-#ifdef FMRX_AB_STOREALL
-    __shared__ float4 sdum[64 + NI / 4];
-#endif
-    const int w = threadIdx.x >> 6, t = threadIdx.x & 63, l = t & (NI - 1), h = t / NI;
+    // the wave (readfirstlane: uniform, so the waves' branches and loops are scalar)
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63, l = t & (NI - 1), h = t / NI;
     const int s = blockIdx.x;  // grid = n_streams
     const float* x = io + (size_t)s * stride;
     float* out = out_base + (size_t)s * ostride;
     const float* S = st + 8 * (size_t)s;
     const float Kp = norm_bw * static_cast<float>(2.666);
     const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
-    PllState p{S[0], S[1], S[2], S[3], S[5]};
+    // the stream's state, uniform over the group (readfirstlane): the domain test below and every
+    // branch and loop after it stay scalar
+    auto uni = [](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v))); };
+    PllState p{uni(S[0]), uni(S[1]), uni(S[2]), uni(S[3]), uni(S[5])};
     // the variant's domain (uniform over the group): NC = 3 from 2^22; NC = 5 with 64-step
     // intervals in [2^21, 2^22), with 16-step ones in [2^20, 2^21)
     if (!(NC == 3 ? pll_pipe_stream(p.trig, step, kPllPipeMin)
@@ -605,31 +612,78 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 }
             }
         };
-        // E2 lanes h = 0: interval k's trigArgs (filter.cpp:165), stored, and checked against
-        // their candidates: a candidate that is not a positive finite float or a threshold
-        // outside its window (-inf) counts as a miss
+        // E2: interval k's check.  Lane group g = t / NB replays batch g of the interval (BPI
+        // batches) from the chain's state before it -- the chain's steps on the same candidate data,
+        // so the same phases -- forms each step's trigArg float(P + phase) (filter.cpp:165) and
+        // checks it against the step's candidates; lane l of the group stores step l's.  A
+        // candidate that is not a positive finite float or a threshold outside its window (-inf)
+        // counts as a miss.  (The chain hands over one state a batch instead of every phase: an
+        // LDS store of four phases cost it ~20 cycles.)
         auto check = [&](int k) {
-            if (w != 2 || h != 0) return;
+            if (w != 2) return;
             const int sl = k & 3;
             if (sexact[sl]) {  // redone exactly: the chain stored it
-                if (l == 0) smiss[sl] = 0;
+                if (t == 0) smiss[sl] = 0;
                 return;
             }
-            const float a = (float)(spr[sl][l] + (double)sph[sl][l]);
-            out[j0(k) + l] = a;
-            const uint32_t cm = scb[sl][l];
-            const float4 tt = sel[sl][l];
+            const int g = t / NB, lg = t & (NB - 1);
+            const bool act = g < BPI;
+            const int gb = act ? g : 0;  // the groups past the interval's batches replay batch 0
+            const float2 r0 = gb > 0 ? sst[sl][gb - 1] : sst[(k - 1) & 3][BPI - 1];
+            float ig = r0.x, ph = r0.y;
+            // step 0's candidate data: those of the trigArg before it (after an exactly redone
+            // interval that trigArg's e in every slot, as the chain's carry)
+            float4 ca, ca2;
+            float cep;
+            if (gb > 0) {
+                ca = sel[sl][NB * gb - 1];
+                cep = sep[sl][NB * gb - 1];
+                ca2 = sel2[NC == 5 ? sl : 0][NC == 5 ? NB * gb - 1 : 0];
+            } else if (sexact[(k - 1) & 3]) {
+                const int j = min(j0(k), n - 1);
+                const float e = pred_e((float)(prs[j0(k) - 1] + (double)ph), x[j], ivs[j]);
+                ca = NC == 3 ? make_float4(0.0f, 0.0f, e, e) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                ca2 = make_float4(e, e, e, e);
+                cep = e;
+            } else {
+                ca = sel[(k - 1) & 3][NI - 1];
+                cep = sep[(k - 1) & 3][NI - 1];
+                ca2 = sel2[NC == 5 ? (k - 1) & 3 : 0][NC == 5 ? NI - 1 : 0];
+            }
+            // the batch's candidate data, read before the steps (the step loop then never waits on
+            // LDS); lane l keeps the phase of step l and checks its own trigArg afterwards
+            float4 da[NB], da2[NC == 5 ? NB : 1];
+            float dep[NB];
+#pragma unroll
+            for (int j = 0; j < NB - 1; j++) {
+                da[j] = sel[sl][NB * gb + j];
+                dep[j] = sep[sl][NB * gb + j];
+                if constexpr (NC == 5) da2[j] = sel2[NC == 5 ? sl : 0][NC == 5 ? NB * gb + j : 0];
+            }
+            float mine = 0.0f;
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                const float e = NC == 3 ? pick(ph, j == 0 ? ca : da[j > 0 ? j - 1 : 0], j == 0 ? cep : dep[j > 0 ? j - 1 : 0])
+                                        : pick5(ph, j == 0 ? ca : da[j > 0 ? j - 1 : 0], j == 0 ? ca2 : da2[NC == 5 && j > 0 ? j - 1 : 0],
+                                                j == 0 ? cep : dep[j > 0 ? j - 1 : 0]);
+                const float2v kv = float2v{Ki, Kp} * e;
+                ig = ig + kv.x;
+                ph = ph + (kv.y + ig);
+                if (j == lg) mine = ph;
+            }
+            const int J = NB * gb + lg;  // this lane's step
+            const float a = (float)(spr[sl][J] + (double)mine);
+            const uint32_t cm = scb[sl][J];
+            const float4 tt = sel[sl][J];
             const float c0 = __builtin_bit_cast(float, cm + (uint32_t)HC);
             const bool thr_ok = tt.x > -__builtin_inff() && tt.y > -__builtin_inff() &&
                                 (NC == 3 || (tt.z > -__builtin_inff() && tt.w > -__builtin_inff()));
             const bool bad = (__builtin_bit_cast(uint32_t, a) - cm > (uint32_t)(NC - 1)) || !thr_ok ||
                              !(c0 > 0.0f && c0 < 3.0e38f);
-            bool any = __builtin_amdgcn_ballot_w64(bad) != 0;
+            if (act) out[j0(k) + J] = a;
+            bool any = __builtin_amdgcn_ballot_w64(act && bad) != 0;
             if (k == min(miss, ni)) any = true;  // test hook: a miss on interval `miss` (the redo path)
-#if defined(FMRX_AB_NOREAD) || defined(FMRX_AB_NOSTORE)
-            any = false;
-#endif
-            if (l == 0) smiss[sl] = any ? 1 : 0;
+            if (t == 0) smiss[sl] = any ? 1 : 0;
         };
 #pragma unroll
         for (int u = 0; u < RD; u++) ld(1 + u, vq[(1 + u) % RD], ivq[(1 + u) % RD], prq[(1 + u) % RD]);
@@ -648,7 +702,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                     if (i <= ni) {
                         const unsigned long long p0 = PROF_T();
                         if (i + 1 <= ni) {
-                            put(i + 1, sph[(i - 1) & 3][NI - 1], vq[sl], ivq[sl], prq[sl]);
+                            put(i + 1, sst[(i - 1) & 3][BPI - 1].y, vq[sl], ivq[sl], prq[sl]);
                             ld(i + 1 + RD, vq[sl], ivq[sl], prq[sl]);
                         }
                         check(i - 1);
@@ -660,7 +714,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                                 float v;
                                 double iv, pr;
                                 ld(i + 1, v, iv, pr);
-                                put(i + 1, sph[(i - 1) & 3][NI - 1], v, iv, pr);
+                                put(i + 1, sst[(i - 1) & 3][BPI - 1].y, v, iv, pr);
                             }
                         }
                         const unsigned long long p1 = PROF_T();
@@ -706,7 +760,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     };
     carry_exact((float)ctx.x, 1);
     if (t == 0) {
-        sph[0][NI - 1] = phase;  // the start of interval 1, for the evaluators' interval 2
+        sst[0][BPI - 1] = make_float2(integ, phase);  // the start of interval 1 (the evaluators' interval 2)
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             smiss[k] = 0;
@@ -722,15 +776,12 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         const int kb = 1 + (i - 1) * BPI;         // the interval's first batch
         // in bursts of CH steps: the data, 1.25 CH (NC = 5: 2.25 CH) 16-byte reads at once in the
         // order the steps need them (spread over the steps they stall the chain more,
-        // tools/ubench_chain.hip), then the steps, then their phases and batch records
+        // tools/ubench_chain.hip), then the steps, then the batch records
         float4 A[CH], A2[NC == 5 ? CH : 1];
         float EP[CH];
         unroll_ic(
             [&](auto hc) {
                 constexpr int H = decltype(hc)::value;
-#ifdef FMRX_AB_NOREAD  // A/B timing only (wrong results): the first burst's data throughout
-                if (i == 1)
-#endif
 #pragma unroll
                 for (int q = 0; q < CH / 4; q++) {
                     *reinterpret_cast<float4*>(&EP[4 * q]) = reinterpret_cast<const float4*>(&sep[is][H * CH])[q];
@@ -740,7 +791,6 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                         if constexpr (NC == 5) A2[4 * q + u] = sel2[NC == 5 ? is : 0][NC == 5 ? H * CH + 4 * q + u : 0];
                     }
                 }
-                float PH[CH];
                 float2 brec[CH / NB];  // (integ, phase) at the end of each batch of the burst
                 unroll_ic(
                     [&](auto gc) {
@@ -758,8 +808,6 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                             chain4_3(phase, integ, kk, a, ep, q);
                         else
                             chain4_5(phase, integ, kk, a, a2, ep, q);
-#pragma unroll
-                        for (int u = 0; u < 4; u++) PH[J + u] = q[u];
                         phase = q[3];
                         if constexpr ((J + 3) % NB == NB - 1) brec[(J + 3) / NB] = make_float2(integ, phase);
                     },
@@ -778,29 +826,13 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 __builtin_amdgcn_sched_barrier(0);
                 __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
                 __builtin_amdgcn_sched_barrier(0);
-#ifdef FMRX_AB_STOREALL  // A/B: the phase stores from every lane, lanes 1-63 to a scratch row
-                {
-                    float4* wp = t == 0 ? reinterpret_cast<float4*>(&sph[is][H * CH]) : &sdum[t];
-#pragma unroll
-                    for (int q = 0; q < CH / 4; q++) wp[q] = *reinterpret_cast<const float4*>(&PH[4 * q]);
-                }
                 if (t == 0) {
 #pragma unroll
-                    for (int q = 0; q < CH / NB; q++) rec[(size_t)s * rb + kb + H * (CH / NB) + q] = brec[q];
+                    for (int q = 0; q < CH / NB; q++) {
+                        sst[is][H * (CH / NB) + q] = brec[q];
+                        rec[(size_t)s * rb + kb + H * (CH / NB) + q] = brec[q];
+                    }
                 }
-#else
-#ifdef FMRX_AB_NOSTORE  // A/B timing only (wrong results): no phase or record stores
-                if (t == 0 && phase == 12345.0f) {
-#else
-                if (t == 0) {
-#endif
-#pragma unroll
-                    for (int q = 0; q < CH / 4; q++)
-                        reinterpret_cast<float4*>(&sph[is][H * CH])[q] = *reinterpret_cast<const float4*>(&PH[4 * q]);
-#pragma unroll
-                    for (int q = 0; q < CH / NB; q++) rec[(size_t)s * rb + kb + H * (CH / NB) + q] = brec[q];
-                }
-#endif
                 carry = A[CH - 1];
                 if constexpr (NC == 5) carry2 = A2[CH - 1];
                 carry_ep = EP[CH - 1];
@@ -822,7 +854,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 const int k0 = 1 + (k - 1) * BPI;
                 exact(q, c, k0, k0 + BPI);
                 if (t == 0) {
-                    sph[k & 3][NI - 1] = q.phase;
+                    sst[k & 3][BPI - 1] = make_float2(q.integ, q.phase);
                     if (k > f) sexact[k & 3] = 1;
                 }
             }
