@@ -531,6 +531,10 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     __shared__ uint32_t scb[4][NI];
     __shared__ double spr[4][NI];
     __shared__ float2 sst[4][BPI];
+    // one batch an interval (the 16-step form): the replay below would be as long as the chain's
+    // own interval, so the chain hands over every phase instead (sph) and wave 2 checks those
+    constexpr bool REPLAY = BPI > 1;
+    __shared__ float sph[REPLAY ? 1 : 4][REPLAY ? 1 : NI];
     __shared__ int smiss[4], sexact[4];
     // the wave (readfirstlane: uniform, so the waves' branches and loops are scalar)
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63, l = t & (NI - 1), h = t / NI;
@@ -624,6 +628,21 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             const int sl = k & 3;
             if (sexact[sl]) {  // redone exactly: the chain stored it
                 if (t == 0) smiss[sl] = 0;
+                return;
+            }
+            if constexpr (!REPLAY) {  // the chain's phases, lanes h = 0
+                const float a = (float)(spr[sl][l] + (double)sph[REPLAY ? 0 : sl][REPLAY ? 0 : l]);
+                if (h == 0) out[j0(k) + l] = a;
+                const uint32_t cm = scb[sl][l];
+                const float4 tt = sel[sl][l];
+                const float c0 = __builtin_bit_cast(float, cm + (uint32_t)HC);
+                const bool thr_ok = tt.x > -__builtin_inff() && tt.y > -__builtin_inff() &&
+                                    (NC == 3 || (tt.z > -__builtin_inff() && tt.w > -__builtin_inff()));
+                const bool bad = (__builtin_bit_cast(uint32_t, a) - cm > (uint32_t)(NC - 1)) || !thr_ok ||
+                                 !(c0 > 0.0f && c0 < 3.0e38f);
+                bool any = __builtin_amdgcn_ballot_w64(h == 0 && bad) != 0;
+                if (k == min(miss, ni)) any = true;  // test hook: a miss on interval `miss` (the redo path)
+                if (t == 0) smiss[sl] = any ? 1 : 0;
                 return;
             }
             const int g = t / NB, lg = t & (NB - 1);
@@ -792,6 +811,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                     }
                 }
                 float2 brec[CH / NB];  // (integ, phase) at the end of each batch of the burst
+                float PH[REPLAY ? 1 : CH];  // (the 16-step form) the burst's phases
                 unroll_ic(
                     [&](auto gc) {
                         constexpr int J = 4 * decltype(gc)::value;  // steps J .. J + 3
@@ -809,6 +829,10 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                         else
                             chain4_5(phase, integ, kk, a, a2, ep, q);
                         phase = q[3];
+                        if constexpr (!REPLAY) {
+#pragma unroll
+                            for (int u = 0; u < 4; u++) PH[REPLAY ? 0 : J + u] = q[u];
+                        }
                         if constexpr ((J + 3) % NB == NB - 1) brec[(J + 3) / NB] = make_float2(integ, phase);
                     },
                     std::make_integer_sequence<int, CH / 4>{});
@@ -827,6 +851,12 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
                 __builtin_amdgcn_sched_barrier(0);
                 if (t == 0) {
+                    if constexpr (!REPLAY) {
+#pragma unroll
+                        for (int q = 0; q < CH / 4; q++)
+                            reinterpret_cast<float4*>(&sph[REPLAY ? 0 : is][REPLAY ? 0 : H * CH])[q] =
+                                *reinterpret_cast<const float4*>(&PH[REPLAY ? 0 : 4 * q]);
+                    }
 #pragma unroll
                     for (int q = 0; q < CH / NB; q++) {
                         sst[is][H * (CH / NB) + q] = brec[q];
