@@ -167,8 +167,11 @@ __global__ void __launch_bounds__(256) pll_prep_kernel(const float* io, int m, i
 // contiguous; the half turns with zero gaps, 2 seg per stream), for the split kernels: a wave there works on at most 4 streams, so stream-minor
 // rows would put every 16-B load of a wave on its own page (rows n_streams x 16 B apart).
 // One thread per sample pair.
+// with_h = 0: no half-turn plane (only pll_spec_lane_kernel reads it; the host passes 0 when that
+// runner is not launched for the segment): 16 B a sample written instead of 32.
 __global__ void __launch_bounds__(256) pll_prep_major_kernel(const float* io, int m, int n_streams, size_t stride,
-                                                             double* side, size_t seg, const float* st, double step) {
+                                                             double* side, size_t seg, const float* st, double step,
+                                                             int with_h) {
     const int s = blockIdx.y;
     const int jp = blockIdx.x * blockDim.x + threadIdx.x;
     if (2 * jp >= m) return;
@@ -183,6 +186,7 @@ __global__ void __launch_bounds__(256) pll_prep_major_kernel(const float* io, in
     const size_t plane = seg * (size_t)n_streams / 2, a = (size_t)s * (seg / 2) + jp;
     siv[a] = iv;
     siv[plane + a] = pr;
+    if (!with_h) return;
     // half turns in 32-B groups (h_2jp, h_2jp+1, 0, 0): pll_spec_lane_kernel's lane 2 reads the
     // first 16 B, the row's other lanes the zeros beside them (same cache line, no mask op)
     double2* sh = siv + 2 * plane + (size_t)s * seg + 2 * (size_t)jp;
@@ -974,7 +978,7 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         float* x = io + off;
         if (spw <= 4)  // the split kernels read stream-major side data
             hipLaunchKernelGGL(pll_prep_major_kernel, dim3(((m + 1) / 2 + 255) / 256, n_streams), dim3(256), 0, s, x, m,
-                               n_streams, stride, side, seg, st, step);
+                               n_streams, stride, side, seg, st, step, (spec && run_lane) ? 1 : 0);
         else
             hipLaunchKernelGGL(pll_prep_kernel, dim3((m + kPrepJ - 1) / kPrepJ, (n_streams + kPrepS - 1) / kPrepS),
                                dim3(256), 0, s, x, m, n_streams, stride, side, seg, st, step);
