@@ -26,7 +26,8 @@
 //           twice the scalar f32 rate on gfx950) and each output is a sequential sum in
 //           ascending tap order with separately rounded mul and add (no FMA), as
 //           filter.cpp:84-92;
-//   demod : neighbour I/Q via LDS, FMDemod in the reference's mixed float/double precision;
+//   demod : neighbour I/Q by a DPP wave shift (LDS for multi-wave workgroups), FMDemod in the
+//           reference's mixed float/double precision;
 //   audio : 51-tap decimating LPF over the demod window in LDS, quantise, store S16.
 #include <hip/hip_runtime.h>
 
@@ -138,7 +139,7 @@ __device__ inline void mono_share(const MonoLaunch& L, int w, int n_chunks, int*
 // TR = 1 keeps the RF taps in VGPRs for the whole launch (the kernel is LDS-capped at two
 // waves per SIMD, which leaves the register file room for them) instead of re-reading them
 // from LDS once per chunk.  Single-wave workgroups (NT = 64) take the demod's neighbour I/Q
-// by lane shuffle, larger ones through LDS.
+// by a DPP wave shift, larger ones through LDS.
 // Measured and dropped: prefetching two chunks ahead, the audio stage once per
 // two chunks in packed ops, a single-buffered demod window with R = 2 for three waves per
 // SIMD, the audio FIR pipelined into the RF tap loop, staggered workgroup starts.
@@ -362,9 +363,13 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
             if (tid == 0) pbuf[cur ^ 1][0] = pbuf[cur][NT];
             prev = pbuf[cur][tid];
         } else {
-            prev.x = __shfl_up(acc[R - 1].x, 1);
-            prev.y = __shfl_up(acc[R - 1].y, 1);
-            if (tid == 0) prev = carry;
+            // lane t - 1's last output by a DPP wave shift (wave_shr:1, one v_mov_b32_dpp a
+            // component, no LDS round trip); lane 0 has no source lane and keeps `old`, the
+            // previous chunk's carry
+            prev.x = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(carry.x), __float_as_int(acc[R - 1].x),
+                                                                0x138, 0xF, 0xF, false));
+            prev.y = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(carry.y), __float_as_int(acc[R - 1].y),
+                                                                0x138, 0xF, 0xF, false));
             carry.x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc[R - 1].x), NT - 1));
             carry.y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc[R - 1].y), NT - 1));
         }
