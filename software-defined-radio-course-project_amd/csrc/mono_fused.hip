@@ -58,6 +58,7 @@ struct MonoCfg {
     static constexpr int slot(int b) { return b + G * (b / S); }
     static constexpr int XB = slot(H + P + 2) + 4;      // LDS pairs
     static constexpr int NLD = (P / 2 + NT - 1) / NT;   // 4-B (2-pair) loads per thread/chunk
+    static constexpr int LH0 = ((P - H) / 2) / NT;      // first load index holding history pairs
     static constexpr int CAmax = (CIF + AD - 1) / AD;   // max audio outputs in one chunk
     static constexpr int NG = (T + 1) / 2;              // tap groups: {0}, {1,2}, {3,4}, ...
     // Audio window (modes 0/1): GA consecutive chunks of demod are gathered before the audio
@@ -251,6 +252,7 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     long long aq = (long long)(c0 - 1) * CIF / AD;
     int ar = (int)((long long)(c0 - 1) * CIF - aq * AD);
     float2v carry = {0.0f, 0.0f};  // NT = 64: last RF output of the previous chunk
+    float4 hist[NLD - C::LH0];     // staged groups of the chunk's last H pairs (loads l >= LH0)
     int slot = -1;                 // audio window slot of chunk c (-1: the pre-roll chunk)
     // modes 2/3: lane t's resampler offset t AD = au_qt AU + au_rt
     const int au_qt = AU > 1 ? tid * AD / AU : 0;
@@ -277,10 +279,10 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                     asm volatile("" ::"v"(w));
                     continue;
                 }
-                if constexpr ((ABL & 8) != 0)
-                    xb4[C::slot(H + 2 * u) / 2] = make_float4(__uint_as_float(w), 0.f, 0.f, 0.f);
-                else
-                    xb4[C::slot(H + 2 * u) / 2] = make_float4(sbyte<0>(w), sbyte<1>(w), sbyte<2>(w), sbyte<3>(w));
+                const float4 f = (ABL & 8) != 0 ? make_float4(__uint_as_float(w), 0.f, 0.f, 0.f)
+                                                : make_float4(sbyte<0>(w), sbyte<1>(w), sbyte<2>(w), sbyte<3>(w));
+                xb4[C::slot(H + 2 * u) / 2] = f;
+                if (l >= C::LH0) hist[l - C::LH0] = f;  // the chunk's last H pairs: next chunk's history
             }
         }
         __syncthreads();  // (A) chunk c staged, carry from c-1 in place
@@ -355,9 +357,14 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         if constexpr (!kShfl) pbuf[cur][tid + 1] = acc[R - 1];
         __syncthreads();  // (B) all RF reads of xb done, pbuf visible
 
-        // ---- carries for chunk c+1: RF history (pairs [P, P+H) -> [0, H)) as aligned 16-B
-        // pair groups (P and H are even, so groups never straddle a pad), last I/Q
-        for (int i = tid; i < H / 2; i += NT) xb4[C::slot(2 * i) / 2] = xb4[C::slot(P + 2 * i) / 2];
+        // ---- carries for chunk c+1: RF history (the chunk's pairs [P - H, P) -> [0, H)) as
+        // aligned 16-B pair groups (P and H are even, so groups never straddle a pad), written
+        // from the staging registers (no LDS read and wait), last I/Q
+#pragma unroll
+        for (int l = C::LH0; l < NLD; l++) {
+            const int i = tid + l * NT - (P - H) / 2;  // history group of staging lane u = tid + l NT
+            if (i >= 0 && ((P / 2) % NT == 0 || tid + l * NT < P / 2)) xb4[C::slot(2 * i) / 2] = hist[l - C::LH0];
+        }
         float2v prev;  // FM demod's previous I/Q: the neighbouring thread's / previous chunk's
         if constexpr (!kShfl) {
             if (tid == 0) pbuf[cur ^ 1][0] = pbuf[cur][NT];
