@@ -107,6 +107,23 @@ __device__ inline float sbyte(uint32_t w) {
     return f;
 }
 
+// The workgroup's LDS hand-offs.  A single-wave workgroup (NT = 64) needs no s_barrier and no
+// drain: a wave's LDS instructions execute in issue order, so a read issued after a write (any
+// lanes) sees it, and every value read into registers is waited for by its own s_waitcnt.
+// Wavefront-scope fences around a wave barrier keep the compiler from moving LDS accesses
+// across the hand-off, without the lgkmcnt(0) a workgroup fence emits.  Larger workgroups take
+// __syncthreads().
+template <int NT>
+__device__ inline void chunk_sync() {
+    if constexpr (NT == 64) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+
 // Workgroup -> (stream, chunk range).  Uniform: segment blockIdx % segs of stream
 // blockIdx / segs.  With L.older_share (> 0, in 1/1024; even segs): the grid is two waves per
 // SIMD, and the hardware dispatches workgroup w into the first wave slot of its SIMD and
@@ -168,7 +185,8 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     __shared__ float dbuf[kWin ? 1 : 2][kWin ? 1 : kAH + CIF];
     __shared__ float2v pbuf[kShfl ? 1 : 2][kShfl ? 1 : NT + 1];  // last RF output per thread
     __shared__ float2 ctab2[TR ? 1 : NG + 1];    // (c[2j-1], c[2j]); c[-1] = 0 (TR = 0 only)
-    __shared__ float atab[kAudioTaps + 1];       // audio taps
+    __shared__ float4 atab4[(kAudioTaps + 3) / 4];  // audio taps, 16-B aligned for broadcast ds_read_b128
+    float* atab = reinterpret_cast<float*>(atab4);
     float* ctab = reinterpret_cast<float*>(ctab2);
     // window sample s (0..49 history, 50.. the GA chunks)
     auto wput = [&](int s, float v) {
@@ -285,7 +303,7 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                 if (l >= C::LH0) hist[l - C::LH0] = f;  // the chunk's last H pairs: next chunk's history
             }
         }
-        __syncthreads();  // (A) chunk c staged, carry from c-1 in place
+        chunk_sync<NT>();  // (A) chunk c staged, carry from c-1 in place
         if (c + 1 < c1) fetch(c + 1);
 
         // ---- RF LPF + decimate.  Thread t owns outputs j = R t + r, r < R, whose samples are
@@ -355,7 +373,7 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
 #pragma unroll
         for (int r = 0; r < R; r++) asm volatile("" ::"v"(acc[r]));
         if constexpr (!kShfl) pbuf[cur][tid + 1] = acc[R - 1];
-        __syncthreads();  // (B) all RF reads of xb done, pbuf visible
+        chunk_sync<NT>();  // (B) all RF reads of xb done, pbuf visible
 
         // ---- carries for chunk c+1: RF history (the chunk's pairs [P - H, P) -> [0, H)) as
         // aligned 16-B pair groups (P and H are even, so groups never straddle a pad), written
@@ -425,7 +443,7 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                 }
             }
         }
-        __syncthreads();  // (C) demod window complete
+        chunk_sync<NT>();  // (C) demod window complete
         // (c+1) CIF = AD aq1 + ar1
         long long aq1 = aq + CIF / AD;
         int ar1 = ar + CIF % AD;
@@ -493,10 +511,25 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                     // base[kAH - k] = (sample o_a - k, sample o_a + DX - k), o_a = woff0 + AD t
                     const float2* base = dwi + woff0 + AD * tid;
                     float2v a2 = {0.0f, 0.0f};
+                    // The taps first (13 broadcast ds_read_b128 from one base + immediates), then
+                    // the window samples kAP taps ahead of their products: the FIR's registers
+                    // are free here, so the loop waits on LDS once instead of every few taps.
+                    constexpr int k0 = (Z0 & 2) ? 1 : 0, k1 = (ABL & 2) != 0 ? 1 : kAudioTaps, kAP = 16;
+                    int zero_a;  // opaque 0: one base VGPR + immediate offsets
+                    asm volatile("v_mov_b32 %0, 0" : "=v"(zero_a));
+                    const float4* at4 = atab4 + zero_a;
+                    float4 tq[(kAudioTaps + 3) / 4];
 #pragma unroll
-                    for (int k = (Z0 & 2) ? 1 : 0; k < ((ABL & 2) != 0 ? 1 : kAudioTaps); k++) {
-                        const float2 xs = base[kAH - k];
-                        const float2v p = float2v{xs.x, xs.y} * atab[k];
+                    for (int q = 0; q < (kAudioTaps + 3) / 4; q++) tq[q] = at4[q];
+                    float2 xs[kAudioTaps];
+#pragma unroll
+                    for (int k = k0; k < k1 && k < k0 + kAP; k++) xs[k] = base[kAH - k];
+#pragma unroll
+                    for (int k = k0; k < k1; k++) {
+                        if (k + kAP < k1) xs[k + kAP] = base[kAH - k - kAP];
+                        const float4 t4 = tq[k / 4];
+                        const float tk = (k & 3) == 0 ? t4.x : (k & 3) == 1 ? t4.y : (k & 3) == 2 ? t4.z : t4.w;
+                        const float2v p = float2v{xs[k].x, xs[k].y} * tk;
                         a2 = a2 + p;
                     }
                     const size_t oi = (size_t)stream * (size_t)n_audio + (size_t)(wm0 + tid);
@@ -508,11 +541,11 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                     }
                 }
                 if (slot == GA - 1) {
-                    __syncthreads();  // window reads done: its last 50 samples become history
+                    chunk_sync<NT>();  // window reads done: its last 50 samples become history
                     // sample GA CIF + i (>= DX) sits in .y of entry GA CIF + i - DX
                     float h = 0.0f;
                     if (tid < kAH) h = dwi[GA * CIF + tid - C::DX].y;
-                    __syncthreads();
+                    chunk_sync<NT>();
                     if (tid < kAH) wput(tid, h);
                 }
             }
