@@ -1,9 +1,9 @@
 #!/bin/bash
 # tools/gpu_r03.sh — the current round-3 GPU check (edited per run; one recipe, not one per run):
-# A/B of the mono kernel: audio FIR with its taps read first and the samples 16 taps ahead (libfmrx.so) vs the per-tap loop
-# (build_ab/, -DFMRX_AB_AUDIO), alternating bench lines on one box; mono/stereo parity tests.
+# A/B of the mono kernel: next chunk staged right after the FIR (libfmrx.so) vs staged at the top of its iteration
+# (build_ab/: the previous commit's source), alternating bench lines on one box; mono/stereo parity tests.
 set -o pipefail
-OUT=gpurun_out/${1:-r03_audio}
+OUT=gpurun_out/${1:-r03_stage}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -k "mono or bench_config or stereo or modes or seek or state" -x -q --timeout 200 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
