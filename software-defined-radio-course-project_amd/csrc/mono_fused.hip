@@ -474,16 +474,25 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                     const int jl = (int)(qb - (long long)c * CIF) + au_qt + wrap;  // j0 - c CIF
                     const float* dw = &dbuf[cur][kAH + jl];
                     const float4* row = reinterpret_cast<const float4*>(L.audio_rows + (size_t)k0 * kAudioRow);
+                    // every load first -- the row's 13 16-B vectors (L2-resident) and the 51
+                    // window samples -- then the sequential sum: one exposed latency per output
+                    // instead of one per few taps (the FIR's registers are free here)
+                    float4 cq[kAudioRow / 4];
+                    float xv[kAudioTaps];
+#pragma unroll
+                    for (int i4 = 0; i4 < kAudioRow / 4; i4++) cq[i4] = row[i4];
+#pragma unroll
+                    for (int i = 0; i < kAudioTaps; i++) xv[i] = dw[-i];
+                    __builtin_amdgcn_sched_barrier(0);
                     float a = 0.0f;
 #pragma unroll
                     for (int i4 = 0; i4 < kAudioRow / 4; i4++) {
-                        const float4 cq = row[i4];
-                        const float cv[4] = {cq.x, cq.y, cq.z, cq.w};
+                        const float cv[4] = {cq[i4].x, cq[i4].y, cq[i4].z, cq[i4].w};
 #pragma unroll
                         for (int e = 0; e < 4; e++) {
                             const int i = 4 * i4 + e;
                             if (i < kAudioTaps) {
-                                const float p = cv[e] * dw[-i];
+                                const float p = cv[e] * xv[i];
                                 a = a + p;
                             }
                         }
