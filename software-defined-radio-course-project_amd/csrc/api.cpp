@@ -274,8 +274,9 @@ int mono_segments(const fmrx_ctx* c, long long n_if) {
 // Unequal shares for the two waves of a SIMD (mono_fused.hip mono_share): when the grid is
 // two resident waves per SIMD (segs even, >= 15/16 of 2 x the SIMD count, 8 workgroups per
 // CU), the first-dispatched wave takes kOlderShare/1024 of each span.  FMRX_MONO_SPLIT=<n>
-// overrides it (0 = equal segments; timing sweeps).
-constexpr int kOlderShare = 620;
+// overrides it (0 = equal segments; timing sweeps).  660 since round 3's latency cuts (sweeps of
+// 580-700 on two boxes, profiles/r03/split_sweep*/: 660 fastest on both, 1.2-1.6 % ahead of 620).
+constexpr int kOlderShare = 660;
 int mono_older_share(const fmrx_ctx* c, int segs) {
     const int n_simd = c->n_simd;
     int share = kOlderShare;

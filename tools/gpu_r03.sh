@@ -1,16 +1,21 @@
 #!/bin/bash
 # tools/gpu_r03.sh — the current round-3 GPU check (edited per run; one recipe, not one per run):
-# A/B of the stereo audio tile kernel: the 51-tap FIR unrolled (libfmrx.so) vs the runtime tap
-# loop (build_ab/, -DFMRX_AB_AUDIOLOOP): kernel-trace stats of configs[4] (256 stereo streams x
-# 60 s) per build; the stereo parity tests.
+# the older wave's share of a SIMD pair's span (FMRX_MONO_SPLIT, in 1/1024; default 620) swept
+# again on the round's final mono kernel: bench lines cycling 620 / 645 / 660 / 675 (second sweep) on one box.
 set -o pipefail
-OUT=gpurun_out/${1:-r03_al}
+OUT=gpurun_out/${1:-r03_split2}
 mkdir -p $OUT
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -k "stereo or bench_config or rds" -x -q --timeout 200 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
-tail -1 $OUT/tests.log
-for i in 1 2; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/new_$i -o run -- python3 tools/bench_stereo.py --streams 256 --seconds 60 > $OUT/new_$i.json 2>&1 || exit 2
-  FMRX_LIB_PATH=$PWD/software-defined-radio-course-project_amd/build_ab/libfmrx.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/old_$i -o run -- python3 tools/bench_stereo.py --streams 256 --seconds 60 > $OUT/old_$i.json 2>&1 || exit 3
+export TMPDIR=/tmp
+for i in 1 2 3; do
+  for sp in 620 645 660 675; do
+    FMRX_MONO_SPLIT=$sp timeout -k 10 120 python bench.py --no-cpu-baseline --no-other-configs > $OUT/s${sp}_$i.json 2> $OUT/s${sp}_$i.err || exit 2
+  done
 done
-grep -h '^{' $OUT/new_*.json $OUT/old_*.json
+OUT=$OUT python - <<'PY'
+import json,glob,os
+out=os.environ["OUT"]
+for sp in (620,645,660,675):
+    r=[json.loads(open(f).read().strip().splitlines()[-1]) for f in sorted(glob.glob(f"{out}/s{sp}_*.json"))]
+    ms=[x["roofline"]["kernel_ms"] for x in r]
+    print(sp, [round(m,4) for m in ms], "mean %.4f" % (sum(ms)/len(ms)))
+PY
