@@ -550,12 +550,14 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
                     }
                 }
                 if (slot == GA - 1) {
-                    chunk_sync<NT>();  // window reads done: its last 50 samples become history
-                    // sample GA CIF + i (>= DX) sits in .y of entry GA CIF + i - DX
-                    float h = 0.0f;
-                    if (tid < kAH) h = dwi[GA * CIF + tid - C::DX].y;
-                    chunk_sync<NT>();
-                    if (tid < kAH) wput(tid, h);
+                    chunk_sync<NT>();  // window reads done: its last 50 samples become history,
+                    // written from this chunk's demod registers (window sample GA CIF + i is
+                    // chunk output jl = CIF - 50 + i) instead of read back from the window
+#pragma unroll
+                    for (int r = 0; r < R; r++) {
+                        const int jl = R * tid + r;
+                        if (jl >= CIF - kAH) wput(jl - (CIF - kAH), d[r]);
+                    }
                 }
             }
         }
