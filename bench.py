@@ -210,10 +210,11 @@ def main() -> None:
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms, launches = rx.kernel_timing(reset=-1)
-    if dist is not None:
-        t = torch.tensor([elapsed, kern_ms], device="cuda" if backend == "nccl" else "cpu", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+    ranks = None
+    if dist is not None:  # every rank's own (seconds, kernel ms): a slow rank shows by name
+        dmod = iqgen.load_module("dist")
+        ranks = dmod.per_rank([elapsed, kern_ms], True, torch.device("cuda", dev))
+        elapsed, kern_ms = max(r[0] for r in ranks), max(r[1] for r in ranks)
 
     total_iq = n_iq * args.steps * world
     value = total_iq / elapsed / 1e6  # IQ Msamples/s, whole job
@@ -286,6 +287,11 @@ def main() -> None:
             line["roofline"]["traffic_note"] = "profiles/traffic_mono101.json is for other kernel sources: not reported"
     line["per_gpu_MS_s"] = round(value / world, 1)
     line["aggregate_MS_s"] = round(value, 1)
+    if ranks is not None:
+        line["dist"] = {"world_size": dist.get_world_size(),
+                        "backend": {"nccl": "RCCL"}.get(dist.get_backend(), dist.get_backend()),
+                        "per_rank": [{"rank": r, "seconds": round(v[0], 4), "kernel_ms": round(v[1], 4)}
+                                     for r, v in enumerate(ranks)]}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:  # the contract: rank 0 at N=1 only
         host = host_info()
@@ -306,6 +312,83 @@ def main() -> None:
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+# Serial-chain floors of the PLL runners (the stereo configs are latency-bound):
+# VALU instructions a step on the runner's critical wave (csrc/pll_pred.hip chain4_3 /
+# chain4_5, stereo.hip pll_spec_lane_kernel, pll_sat.hip) x ~4.2 cycles a wave64 VALU issue on
+# gfx950 (tools/ubench_dep.hip, profiles/r03/ubench_dep.txt), at the 2.4 GHz peak engine clock
+CHAIN_VALU_PER_STEP = {"runner_lane": 35.5, "runner_pred": 16.0, "runner_sat": 8.0, "runner_pipe20": 12.0,
+                       "runner_pipe21": 12.0, "runner_pipe22": 9.0}
+VALU_ISSUE_CYCLES = 4.2
+PEAK_CLOCK_GHZ = 2.4
+
+
+def stage_latency(rx, run) -> dict:
+    """One more call of `run` with fmrx_debug_stage_timing armed: device ms per stage of the
+    stereo engine and, per PLL runner regime, ns per serial step against the chain's
+    instruction floor (CHAIN_VALU_PER_STEP)."""
+    rx.reset()
+    rx.stage_timing(1)
+    run()
+    rx.synchronize()
+    st = rx.stage_timing(-1)
+    stages = {k: round(v[0], 3) for k, v in st.items()}
+    regimes = {}
+    for k, (ms, _, steps) in st.items():
+        if steps > 0 and k in CHAIN_VALU_PER_STEP:
+            ns = ms * 1e6 / steps
+            floor = CHAIN_VALU_PER_STEP[k] * VALU_ISSUE_CYCLES / PEAK_CLOCK_GHZ
+            regimes[k] = {"steps_per_stream": int(steps), "ns_per_step": round(ns, 2),
+                          "floor_ns_per_step": round(floor, 2), "frac": round(floor / ns, 3)}
+    runner_ms = sum(v[0] for k, v in st.items() if k.startswith("runner_"))
+    return {"bound": "serial PLL chain (one recurrence a stream)", "stage_ms": stages,
+            "runner_ms": round(runner_ms, 2), "non_runner_ms": round(sum(v[0] for v in st.values()) - runner_ms, 2),
+            "regimes": regimes,
+            "floor_note": f"chain VALU a step x {VALU_ISSUE_CYCLES} cycles at {PEAK_CLOCK_GHZ} GHz "
+                          "(bench.CHAIN_VALU_PER_STEP); stage ms from HIP events, overlapping stages add up"}
+
+
+def cpu_reference_stereo(host_iq, gpu_pcm) -> dict:
+    """SURVEY §8d CPU plan for configs[2]: the reference's own stereo path (oracle/_ref: the
+    sequential project.cpp driver over src/filter.cpp, 1 core) on the same 1 GiB, and the
+    reference's two-thread `project 0 2` executable reading it on stdin (it exits at EOF with
+    blocks still queued, project.cpp:51-54, so its PCM is compared as a prefix)."""
+    import hashlib
+    import subprocess
+    import tempfile
+
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    if not oracle.reference_available():
+        return {"error": "oracle/_ref not built"}
+    nb = host_iq.size // 12800
+    t0 = time.perf_counter()
+    pcm = oracle.Reference().run(0, 51, host_iq, ["pcm"])["pcm"]
+    dt = time.perf_counter() - t0
+    out = {"value": round(host_iq.size / 2 / dt / 1e6, 2), "unit": "MS/s", "cores": 1, "kind": "reference",
+           "sample": f"the same {nb} blocks, sequential project.cpp order (oracle/_ref)", "seconds": round(dt, 3),
+           "x_realtime": round(host_iq.size / 2 / RT_RATE / dt, 1),
+           "bit_exact_vs_gpu": hashlib.sha256(pcm.tobytes()).hexdigest() == hashlib.sha256(gpu_pcm.tobytes()).hexdigest()}
+    exe = os.path.join(REPO, "oracle", "_ref", "project")
+    if os.path.exists(exe):
+        with tempfile.TemporaryDirectory(dir="/tmp") as d:
+            src, dst = os.path.join(d, "iq.u8"), os.path.join(d, "pcm.s16")
+            host_iq.tofile(src)
+            with open(src, "rb") as fi, open(dst, "wb") as fo:
+                t0 = time.perf_counter()
+                subprocess.run([exe, "0", "2"], stdin=fi, stdout=fo, stderr=subprocess.DEVNULL, timeout=120)
+                dt = time.perf_counter() - t0
+            got = np.fromfile(dst, np.int16)
+        out["threaded_project"] = {
+            "seconds": round(dt, 3), "x_realtime": round(host_iq.size / 2 / RT_RATE / dt, 1), "cores": 2,
+            "blocks_written": int(got.size // 256),
+            "prefix_bit_exact_vs_gpu": bool(got.size > 0 and np.array_equal(got, gpu_pcm[: got.size])),
+            "sample": "src/project.cpp built as src/Makefile (oracle/_ref/project 0 2), stdin -> file"}
+    return out
 
 
 def other_configs(fmrx) -> dict:
@@ -335,10 +418,14 @@ def other_configs(fmrx) -> dict:
         out["configs[2]"] = {"workload": f"mode-0 stereo (REF_EXACT), one stream, 1 GiB ({nb} blocks) in one call",
                              "seconds": round(dt, 3), "MS_per_s": round(nb * bb / 2 / dt / 1e6, 1),
                              "x_realtime": round(sig / dt, 1)}
-        out["configs[2]"].update(parity_vs_reference("bench_c2_m0_stereo_gib", iq, pcm))
+        par, host_iq, host_pcm = parity_vs_reference("bench_c2_m0_stereo_gib", iq, pcm, keep=True)
+        out["configs[2]"].update(par)
+        out["configs[2]"]["latency"] = stage_latency(rx, lambda: rx.process_device(iq.data_ptr(), nb, pcm.data_ptr()))
         rx.close()
         del iq, pcm
         torch.cuda.empty_cache()
+        out["configs[2]"]["cpu_baseline"] = cpu_reference_stereo(host_iq, host_pcm)
+        del host_iq, host_pcm
         rx = fmrx.Receiver(2, fmrx.MONO)
         bb = rx.geo.block_bytes
         nb = STREAM_BYTES // bb
@@ -347,26 +434,64 @@ def other_configs(fmrx) -> dict:
         rx.synth_device(3001, 0, nb * bb // 2, iq.data_ptr())
         warm_up(lambda: rx.process_device(iq.data_ptr(), nb, pcm.data_ptr()), rx.synchronize, 2, 1.0)
         steps = 10
+        rx.kernel_timing(reset=1)
         t0 = time.perf_counter()
         for _ in range(steps):
             rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
         rx.synchronize()
         dt = (time.perf_counter() - t0) / steps
+        kms, _ = rx.kernel_timing(reset=-1)
+        na = rx.geo.audio_frames
+        n_iq = nb * bb // 2
+        alg = nb * bb + 2 * nb * na  # u8 I+Q in, S16 mono out (2.037 B/IQ)
+        # flop per IQ (mul and add apart): RF 51 taps x 2 channels / decimation 10,
+        # demod ~0.9, the resampler's 51 taps per output at 18,816 outputs per 1,024,000 IQ
+        fl = 2 * 51 * 2 / 10 + 0.9 + 51 * 2 * na / (bb // 2)
         out["configs[3]"] = {"workload": f"mode-2 mono, 147/800 polyphase resampler, 1 GiB ({nb} blocks)",
                              "ms_per_step": round(dt * 1e3, 4), "MS_per_s": round(nb * bb / 2 / dt / 1e6, 1),
-                             "x_realtime": round(nb * bb / 2 / rx.geo.rf_fs / dt, 1)}
+                             "x_realtime": round(nb * bb / 2 / rx.geo.rf_fs / dt, 1),
+                             "roofline": {"bound": "hbm", "kernel": "mono_fused_kernel<51,10,AU=147>",
+                                          "kernel_ms": round(kms, 4), "alg_bytes_per_launch": alg,
+                                          "achieved": round(alg / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                                          "unit": "GB/s", "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                          "binding": {"bound": "valu_f32_no_fma", "flop_per_iq": round(fl, 2),
+                                                      "achieved": round(fl * n_iq / (kms * 1e-3) / 1e12, 2),
+                                                      "peak": VALU_F32_PEAK_TOPS, "unit": "Tflop/s",
+                                                      "frac": round(fl * n_iq / (kms * 1e-3) / 1e12 / VALU_F32_PEAK_TOPS, 4)}}}
         # the timed steps carried state from step to step: the parity pass starts fresh
         rx.reset()
         rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
         rx.synchronize()
-        out["configs[3]"].update(parity_vs_reference("bench_c3_m2_mono_gib", iq, pcm))
+        par, host_iq, host_pcm = parity_vs_reference("bench_c3_m2_mono_gib", iq, pcm, keep=True)
+        out["configs[3]"].update(par)
         rx.close()
+        del iq, pcm
+        torch.cuda.empty_cache()
+        out["configs[3]"]["cpu_baseline"] = cpu_reference_mono2(host_iq, host_pcm)
     except Exception as e:  # the headline line must still print
         out["error"] = repr(e)
     return out
 
 
-def parity_vs_reference(key: str, d_iq, d_pcm) -> dict:
+def cpu_reference_mono2(host_iq, gpu_pcm) -> dict:
+    """configs[3]'s CPU baseline: the reference's mode-2 mono path (oracle/_ref, src/filter.cpp's
+    resample with up 147 / down 800, 1 core, sequential) on the same 1 GiB."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    if not oracle.reference_available():
+        return {"error": "oracle/_ref not built"}
+    t0 = time.perf_counter()
+    pcm = oracle.Reference().run_mono(2, 51, host_iq)
+    dt = time.perf_counter() - t0
+    return {"value": round(host_iq.size / 2 / dt / 1e6, 2), "unit": "MS/s", "cores": 1, "kind": "reference",
+            "sample": f"the same {host_iq.size // 2048000} blocks, sequential mono path (oracle/_ref)",
+            "seconds": round(dt, 3), "bit_exact_vs_gpu": bool(np.array_equal(pcm, gpu_pcm))}
+
+
+def parity_vs_reference(key: str, d_iq, d_pcm, keep: bool = False):
     """Full-size parity of an extra config, after its timing: SHA-256 of the bench's input and
     of the GPU's PCM against the reference build's over the same bytes (tests/golden/hashes.json
     `bench_*`, written by tests/golden/make_golden.py --bench-only through oracle/_ref)."""
@@ -374,12 +499,14 @@ def parity_vs_reference(key: str, d_iq, d_pcm) -> dict:
 
     with open(os.path.join(REPO, "tests", "golden", "hashes.json")) as f:
         want = json.load(f)[key]
-    got_in = hashlib.sha256(d_iq.cpu().numpy().tobytes()).hexdigest()
-    got_pcm = hashlib.sha256(d_pcm.cpu().numpy().tobytes()).hexdigest()
-    return {"input_matches_fixture": got_in == want["input_sha256"],
-            "bit_exact_vs_reference": got_in == want["input_sha256"] and got_pcm == want["pcm_sha256"],
-            "parity_source": f"tests/golden/hashes.json {key}: reference build (oracle/_ref) "
-                             f"{want['field']} SHA-256 over the same {want['n_blocks']} blocks"}
+    h_iq, h_pcm = d_iq.cpu().numpy(), d_pcm.cpu().numpy()
+    got_in = hashlib.sha256(h_iq.tobytes()).hexdigest()
+    got_pcm = hashlib.sha256(h_pcm.tobytes()).hexdigest()
+    res = {"input_matches_fixture": got_in == want["input_sha256"],
+           "bit_exact_vs_reference": got_in == want["input_sha256"] and got_pcm == want["pcm_sha256"],
+           "parity_source": f"tests/golden/hashes.json {key}: reference build (oracle/_ref) "
+                            f"{want['field']} SHA-256 over the same {want['n_blocks']} blocks"}
+    return (res, h_iq, h_pcm) if keep else res
 
 
 def streams_config(fmrx, world: int, rank: int, dev: int, seconds: float) -> dict | None:
@@ -393,9 +520,11 @@ def streams_config(fmrx, world: int, rank: int, dev: int, seconds: float) -> dic
     import torch
 
     dmod = iqgen.load_module("dist")
-    expect = iqgen.stream_hashes(256, int(seconds * RT_RATE * 2 // 12800)) or None
-    try:
-        res = dmod.streams_leg(fmrx, 256, seconds, world, rank, dev, expect=expect)
+    # the same geometry streams_leg sizes its run from (mode 0 stereo)
+    geo = fmrx.geometry(fmrx.default_config(0, fmrx.STEREO))
+    expect = iqgen.stream_hashes(256, int(seconds * geo.rf_fs * 2 // geo.block_bytes)) or None
+    try:  # streams_leg agrees on failure across ranks before each collective (dist.run_leg)
+        res = dmod.streams_leg(fmrx, 256, seconds, world, rank, dev, expect=expect, profile=stage_latency)
     except Exception as e:  # the headline line must still print
         res = {"error": repr(e)} if rank == 0 else None
     torch.cuda.empty_cache()

@@ -215,6 +215,16 @@ int fmrx_debug_mono_stamps(fmrx_ctx* ctx, unsigned long long* d_stamps, size_t n
  * d_counts[1].  Results are unchanged.  d_counts = NULL turns it off.                          */
 int fmrx_debug_pll_stats(fmrx_ctx* ctx, unsigned long long* d_counts);
 
+/* ---- diagnostic: per-stage device time of the stereo engine ------------------------------ */
+/* op 1 arms (and clears) HIP event pairs around every stage launch of the following stereo     *
+ * calls (ms of overlapping stages add up); op 0 reads, op -1 reads and disarms.  Stage k of     *
+ * n_kinds: 0 RF front end, 1 band-pass pair, 2 PLL pre-pass, 3 lane runner, 4 two-wave          *
+ * predicted runner, 5 saturated runner, 6/7/8 three-wave runner forms from trigOffset 2^20 /   *
+ * 2^21 / 2^22, 9 check, 10 resume/tail, 11 NCO, 12 audio.  ms[k] = summed device time,          *
+ * launches[k] = launches, steps[k] = serial PLL steps a runner kind ran as its segment's only  *
+ * runner (per stream chain; for ns per step of each regime).  Results are unchanged.           */
+int fmrx_debug_stage_timing(fmrx_ctx* ctx, int op, double* ms, double* steps, long* launches, int n_kinds);
+
 #ifdef __cplusplus
 }
 #endif

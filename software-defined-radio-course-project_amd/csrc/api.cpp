@@ -120,6 +120,7 @@ struct fmrx_ctx {
     bool timing = false;
     unsigned long long* stamps = nullptr;  // fmrx_debug_mono_stamps (diagnostic)
     unsigned long long* pll_stats = nullptr;  // fmrx_debug_pll_stats (diagnostic)
+    StageTimer stage_timer;                   // fmrx_debug_stage_timing (diagnostic)
     int n_simd = 1024;                        // SIMDs of cfg.device (4 per CU), set at creation
     // bounds on the streams' trigOffset (PllHint) of the stereo and the RDS PLL: 0 after a reset,
     // advanced by every call's samples (the float increments stick at 2^24), re-read from the
@@ -138,6 +139,7 @@ struct fmrx_ctx {
         h.known = t.known;
         h.trig_lo = t.lo;
         h.trig_hi = t.hi;
+        h.timer = stage_timer.on ? const_cast<StageTimer*>(&stage_timer) : nullptr;
         return h;
     }
 };
@@ -333,8 +335,10 @@ int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
         ev = &c->evs[c->ev_used++];
         HIPCHK(hipEventRecord(ev->first, c->stream));
     }
+    const int st_t = (!with_audio && d_demod) ? c->stage_timer.begin(c->stream) : -1;
     int rc = launch_mono_fused(L, ns, c->geo.rf_taps, c->geo.rf_decim, c->geo.audio_up,
                                c->geo.audio_up == 1 ? ad : c->geo.audio_down, c->mono_taps, c->stream);
+    c->stage_timer.end(st_t, kStFront, 0.0, c->stream);
     if (rc != 0) return fail(rc == -1 ? FMRX_EINVAL : FMRX_EHIP, "fused kernel launch failed (%d)", rc);
     if (ev) HIPCHK(hipEventRecord(ev->second, c->stream));
     if (with_audio) c->audio_hist_stale = false;  // demod_tail rewrote the audio history
@@ -395,7 +399,9 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
     S.ch_c = c->ch.data();
     S.ca_c = c->ca.data();
     S.bp_taps = c->geo.bp_taps;
+    const int t_bp = c->stage_timer.begin(c->stream);
     if (launch_bpf_pair(S, ns, c->stream)) return fail(FMRX_EHIP, "band-pass launch failed");
+    c->stage_timer.end(t_bp, kStBpf, 0.0, c->stream);
     // project.cpp:166: PLL(carrier, 19000, if_fs, 2, 0, 0.01, ...)
     if ((rc = c->d_pll_side.ensure(pll_side_doubles((int)n_if, ns)))) return rc;
     if (launch_pll(c->d_carrier.p, (int)n_if, ns, n_if, 19000.0f, (float)c->geo.if_fs, 2.0f, 0.0f,
@@ -421,7 +427,9 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
     A.down = c->geo.audio_down;
     A.at = c->geo.audio_taps_total;
     A.audio_c = c->d_audio.p;
+    const int t_au = c->stage_timer.begin(c->stream);
     if (launch_stereo_audio(A, ns, c->stream)) return fail(FMRX_EHIP, "stereo audio launch failed");
+    c->stage_timer.end(t_au, kStAudio, 0.0, c->stream);
     // demod history for the next call: last kDemodHist samples -> front, every stream in one
     // launch (n_if >= one block of IF samples > kDemodHist: the ranges never overlap)
     if (launch_copy_streams(c->d_demod.p, c->demod_stride, c->d_demod.p + n_if, c->demod_stride, kDemodHist, ns,
@@ -609,6 +617,7 @@ void fmrx_destroy(fmrx_ctx* c) {
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
     }
+    c->stage_timer.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -778,7 +787,14 @@ int fmrx_process_device(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16
 int fmrx_synchronize(fmrx_ctx* c) {
     CtxLock lock_(c);
     if (!c) return fail(FMRX_EINVAL, "null context");
-    HIPCHK(hipStreamSynchronize(c->stream));
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+        // an asynchronous fault of an enqueued launch: the device state no longer follows the
+        // host's trigOffset bounds, so the runner choice falls back to "unknown" until a reset
+        c->pll_trig.known = false;
+        c->rds_trig.known = false;
+        return fail(FMRX_EHIP, "stream synchronize failed: %s", hipGetErrorString(e));
+    }
     return FMRX_OK;
 }
 
@@ -1014,8 +1030,17 @@ int fmrx_pll(fmrx_ctx* c, float* d_io, int n, float freq, float fs, float nco_sc
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(c->d_scratch.p, d_st, 6 * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
     if ((rc = c->d_pll_side.ensure(pll_side_doubles(n, 1)))) return rc;
-    PllHint hint;  // the state is the caller's: trigOffset unknown
+    // the state is the caller's: its trigOffset (read back, 4 bytes) is the hint when it is in the
+    // float increments' domain (an integer in [0, 2^24]); unknown otherwise (every runner launched
+    // for every segment, each taking its own streams)
+    float trig = -1.0f;
+    HIPCHK(hipMemcpyAsync(&trig, d_st + 5, sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    PllHint hint;
     hint.n_simd = c->n_simd;
+    hint.known = trig >= 0.0f && trig <= 16777216.0f && trig == std::floor(trig);
+    hint.trig_lo = hint.trig_hi = hint.known ? (double)trig : 0.0;
+    hint.timer = c->stage_timer.on ? &c->stage_timer : nullptr;
     if (launch_pll(d_io, n, 1, (size_t)n, freq, fs, nco_scale, phase_adjust, norm_bw, c->d_scratch.p,
                    c->d_pll_side.p, c->stream, hint, c->pll_stats))
         return fail(FMRX_EHIP, "launch failed");
@@ -1090,8 +1115,10 @@ int fmrx_synth_device(fmrx_ctx* c, uint64_t seed, int rf_fs, uint64_t first_pair
 int fmrx_synth_device_streams(fmrx_ctx* c, const uint64_t* seeds, size_t n_seeds, int rf_fs, uint64_t first_pair,
                               size_t n_pairs, uint8_t* d_out, size_t stride_bytes) {
     CtxLock lock_(c);
+    // synth_streams_kernel stores 16-bit (I, Q) pairs at d_out + k stride: both must be even
     if (!c || !d_out || !seeds || rf_fs <= 0 || n_seeds == 0 || n_seeds > 65535 ||
-        (n_seeds > 1 && stride_bytes < 2 * n_pairs) || (stride_bytes & 1))
+        (n_seeds > 1 && stride_bytes < 2 * n_pairs) || (stride_bytes & 1) ||
+        (reinterpret_cast<uintptr_t>(d_out) & 1))
         return fail(FMRX_EINVAL, "bad argument");
     int rc = set_device(c);
     if (rc) return rc;
@@ -1102,8 +1129,10 @@ int fmrx_synth_device_streams(fmrx_ctx* c, const uint64_t* seeds, size_t n_seeds
     HIPCHK(hipMemcpyAsync(c->d_synth_params.p, ps.data(), sizeof(SynthParams) * n_seeds, hipMemcpyHostToDevice,
                           c->stream));
     if (launch_synth_streams(reinterpret_cast<const SynthParams*>(c->d_synth_params.p), (int)n_seeds,
-                             c->d_sintab.p, first_pair, n_pairs, d_out, stride_bytes, c->stream))
+                             c->d_sintab.p, first_pair, n_pairs, d_out, stride_bytes, c->stream)) {
+        (void)hipStreamSynchronize(c->stream);  // the copy from ps may still be in flight
         return fail(FMRX_EHIP, "synth launch failed");
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
     return FMRX_OK;
 }
@@ -1119,6 +1148,42 @@ int fmrx_debug_mono_stamps(fmrx_ctx* c, unsigned long long* d_stamps, size_t n_w
     if (d_stamps && needed && n_workgroups < *needed)
         return fail(FMRX_EINVAL, "stamp buffer holds %zu workgroups, up to %zu launch", n_workgroups, *needed);
     c->stamps = d_stamps;
+    return FMRX_OK;
+}
+
+// Diagnostic: per-stage device time of the stereo engine (StageTimer).  op 1 arms (and clears),
+// 0 reads, -1 reads and disarms; the read waits for the last recorded event.
+int fmrx_debug_stage_timing(fmrx_ctx* c, int op, double* ms, double* steps, long* launches, int n_kinds) {
+    CtxLock lock_(c);
+    if (!c) return fail(FMRX_EINVAL, "null context");
+    int rc = set_device(c);
+    if (rc) return rc;
+    StageTimer& T = c->stage_timer;
+    if (op == 1) {
+        T.on = true;
+        T.used = 0;
+        return FMRX_OK;
+    }
+    if (n_kinds < 0 || (n_kinds > 0 && (!ms || !steps || !launches))) return fail(FMRX_EINVAL, "bad argument");
+    for (int k = 0; k < n_kinds; k++) {
+        ms[k] = steps[k] = 0.0;
+        launches[k] = 0;
+    }
+    if (T.used) HIPCHK(hipEventSynchronize(T.recs[T.used - 1].b));
+    for (size_t i = 0; i < T.used; i++) {
+        const StageTimer::Rec& r = T.recs[i];
+        if (r.kind >= n_kinds) continue;
+        float t = 0.0f;
+        HIPCHK(hipEventSynchronize(r.b));
+        HIPCHK(hipEventElapsedTime(&t, r.a, r.b));
+        ms[r.kind] += t;
+        steps[r.kind] += r.steps;
+        launches[r.kind] += 1;
+    }
+    if (op == -1) {
+        T.on = false;
+        T.used = 0;
+    }
     return FMRX_OK;
 }
 

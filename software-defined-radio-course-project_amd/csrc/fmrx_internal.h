@@ -5,6 +5,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "mono_launch.h"
 #include "synth.h"
 
@@ -50,10 +52,55 @@ size_t pll_side_doubles(int n, int n_streams);
 // start (integer-valued, <= 2^24: the reference's float increments from a reset), so that
 // launch_pll enqueues only the runners some segment can use.  Unknown (the fmrx_pll primitive's
 // state lives in caller memory): every runner is launched and each takes its own waves.
+// Per-stage device time of the stereo engine (fmrx_debug_stage_timing; diagnostic): HIP event
+// pairs recorded on the stream each stage is launched on, read after the call.  Runner records
+// carry the serial steps they ran when they were the only runner of their segment (the host's
+// trigOffset bounds put every stream in that runner's regime), so ns per step per regime is
+// measured, not modelled.
+enum StageKind {
+    kStFront, kStBpf, kStPrep, kStLane, kStPred, kStSat, kStPipe20, kStPipe21, kStPipe22, kStCheck, kStTail,
+    kStNco, kStAudio, kStKinds
+};
+struct StageTimer {
+    bool on = false;
+    struct Rec {
+        int kind;
+        double steps;
+        hipEvent_t a, b;
+    };
+    std::vector<Rec> recs;
+    size_t used = 0;
+    int begin(hipStream_t s) {
+        if (!on) return -1;
+        if (used == recs.size()) {
+            Rec r{0, 0.0, nullptr, nullptr};
+            if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return -1;
+            recs.push_back(r);
+        }
+        if (hipEventRecord(recs[used].a, s) != hipSuccess) return -1;
+        return (int)used++;
+    }
+    void end(int i, int kind, double steps, hipStream_t s) {
+        if (i < 0) return;
+        recs[i].kind = kind;
+        recs[i].steps = steps;
+        (void)hipEventRecord(recs[i].b, s);
+    }
+    void release() {
+        for (auto& r : recs) {
+            (void)hipEventDestroy(r.a);
+            (void)hipEventDestroy(r.b);
+        }
+        recs.clear();
+        used = 0;
+    }
+};
+
 struct PllHint {
     int n_simd = 1024;
     bool known = false;
     double trig_lo = 0.0, trig_hi = 0.0;
+    StageTimer* timer = nullptr;  // diagnostic stage timing (null: off)
 };
 int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
                float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s,
@@ -72,14 +119,17 @@ void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_str
                      const double* side, size_t seg, double step, float norm_bw, const float* st, float* out,
                      size_t ostride, int* fail, float2* rec, size_t rb, int inject, int sat_ok, int pipe_on);
 // pll_pred.hip: the three-wave runner for one stream a workgroup (spw == 1) from trigOffset 2^20,
-// the stick included (pll_pipe_stream): `from22` launches its form for the streams from 2^22 (3
-// candidates, 64-step intervals), `from21` the one for [2^21, 2^22) (5 candidates, 64 steps),
-// `from20` the one for [2^20, 2^21) (5 candidates, 16 steps); launched, they take those streams
-// from the pred and saturated runners.  miss >= 1 (test hook): the check reports a miss on that
-// interval (the last one if past it), so the exact redo runs
-void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_t stride, const double* side,
-                     size_t seg, double step, float norm_bw, const float* st, float* out, size_t ostride, int* fail,
-                     float2* rec, size_t rb, int inject, int miss, bool from22, bool from21, bool from20);
+// the stick included (pll_pipe_stream), self-certifying (no check / resume kernel): one launch runs
+// samples [0, n) of io (stream stride `stride`) from the state st and writes their trigArgs to out
+// (stride ostride) and the exact end state to st.  form 22: 3 candidates, 64-step intervals
+// (trigOffset from 2^22); 21: 5 candidates, 64 steps ([2^21, 2^22)); 20: 5 candidates, 16 steps
+// ([2^20, 2^21)).  A stream whose trigOffset is outside the form's domain runs the range on the
+// exact path (a wrong host hint costs speed, not bits).  miss >= 1 / inject >= 0 (test hooks):
+// a forced miss on interval `miss` / interval 1 + (inject + s) % intervals, so the exact redo
+// runs.  stats (may be null): += batches redone exactly, batches run.
+void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
+                     float* st, float* out, size_t ostride, int inject, int miss, int form,
+                     unsigned long long* stats);
 
 // test hook: the PLL's fallback libm on device (kind 0 sincos, 1 atan2, 2 NCO cos)
 int launch_pll_fallback_test(int kind, const float* a, const float* b, size_t n, float* out, hipStream_t s);

@@ -486,29 +486,90 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
 // masks, v_cndmask), (Ki e, Kp e), the three float updates: 9 instructions a step with NC = 3
 // candidates, 12 with 5, four steps an asm block (chain4_3 / chain4_5) -- and hands one state a
 // batch, (integ, phase) after its last step, to the other waves:
-//   wave 1: interval k + 1's e for the NC candidates c0 - NC/2 .. c0 + NC/2 of every step;
+//   wave 1: interval k + 1's e for the NC candidates c0 - NC/2 .. c0 + NC/2 of every step, each
+//           with its certification (pred_e_cert: the float roundings of the candidate's sin/cos
+//           and of atan2 proven as in pll_batch_fast);
 //   wave 2: interval k + 1's NC - 1 phase thresholds a step, c0's bits and P; and interval
 //           k - 1 replayed batch by batch from those states, one lane group a batch (the chain's
 //           arithmetic on the same data, so the same phases), its trigArgs float(P + phase)
-//           (filter.cpp:165), their check against the candidates and the output stores.
+//           (filter.cpp:165), their check against the candidates AND the certification of the
+//           candidate each step took, and the output stores.
+// So the runner is exact by construction: every e the chain used is the exact path's e (a
+// certified candidate that is the true trigArg), every state it carries is the exact path's.  No
+// pll_check_kernel, no resume kernel, no pre-pass (1/v and P = step x trigOffset are formed
+// inline, pll_side's arithmetic): one launch runs a form's whole range of the call, however long,
+// and leaves the exact end state in st.
 // The candidates of interval k + 1 come from the phase at the start of interval k
 // (tools/pll_predict.cpp, lookback 2).  NC = 3 with 64-step intervals from 2^22 (every interval
 // of the bench stream hit), NC = 5 with 64-step intervals in [2^21, 2^22) (99.97 %) and with
 // 16-step ones in [2^20, 2^21) (99.7 %).  The chain reads an interval's data in bursts before
 // their steps (spread over the steps the reads stall it more: tools/ubench_chain.hip,
-// profiles/r03/ubench_chain.txt).  A missed interval -- wave 2 flags it in the interval after the
-// chain ran it, the chain reads the flag at the end of the next one -- is redone on the exact
-// path with the two after it (pll_redo from the recorded state); every wave takes two more
-// barriers around that redo, and the evaluators redo the next interval from the corrected
-// phase.  The output goes through pll_check_kernel like every runner's.
+// profiles/r03/ubench_chain.txt).  A missed interval (a trigArg outside its candidates, or taken
+// from an uncertified one) -- wave 2 flags it in the interval after the chain ran it, the chain
+// reads the flag at the end of the next one -- is redone on the exact path with the two after it
+// (pll_redo from the state at the interval's start, kept in the LDS ring); every wave takes two
+// more barriers around that redo, and the evaluators redo the next interval from the corrected
+// phase.
+
+// pred_e with pll_batch_fast's certification of one step: the float roundings of the
+// candidate's cos and sin (16-ulp margin), |r| >= kPllMinR, |a| < kPllMaxX, [th - E, th + E]
+// within one float (E = kPllEBatch: d = Y iv with the rcp-Newton 1/v), |d| < kPllMaxD, |B| <=
+// kPllMaxB, a finite iv.  ok: e is then the exact path's e (pll_step, glibc's atan2 rounded) for
+// a step with input v after trigArg a, bit for bit.
+__device__ inline float pred_e_cert(float a, float v, double iv, bool& ok) {
+    const double x = (double)a;
+    const double nd = rint(x * kInvPio2);
+    const double r = fma(-nd, kPio2Lo, fma(-nd, kPio2Hi, x));
+    const double z = r * r;
+    const double sn = r * split_w_horner(z, split_coef(false));
+    const double cs = split_w_horner(z, split_coef(true));
+    const float fc = (float)cs, nfs = -(float)sn;
+    const float2v ab = float2v{fc, nfs} * v;
+    const double Y = fma((double)ab.x, sn, (double)ab.y * cs);
+    const double h = iv < 0.0 ? 0.5 : 0.0;
+    const double B = pll_offset_h(x, h);
+    const double d = Y * iv;
+    const double th = d + B;
+    const float lo = (float)(th - kPllEBatch), hi = (float)(th + kPllEBatch);
+    ok = (int)(fabs(x) < kPllMaxX) & (int)(pll_margin16x8(cs) > 256u) & (int)(pll_margin16x8(sn) > 256u) &
+         (int)(fabs(r) >= kPllMinR) & (int)(lo == hi) & (int)(fabs(d) < kPllMaxD) & (int)(fabs(B) <= kPllMaxB);
+    return lo;
+}
+
+// 1 / v as the check kernel forms it (reciprocal + one Newton step, ~2^-46 relative, within the
+// batch bound kPllEBatch); NaN outside [kPllMinV, 1e300) (pll_side)
+__device__ inline double pll_iv(float v) {
+    const double vd = (double)v;
+    const double r0 = __builtin_amdgcn_rcp(vd);
+    const double r1 = fma(r0, fma(-vd, r0, 1.0), r0);
+    return (fabs(vd) >= (double)kPllMinV && fabs(vd) < 1.0e300) ? r1 : (double)NAN;
+}
+
+// The exact path's e of a step with input v whose previous trigArg is a (pll_step's first half
+// from the state after that trigArg: its sin/cos certified or from the library, then the
+// rotation atan2 certified or from the library).  Used where the chain continues after an exact
+// stretch, by the chain and by wave 2's replay alike.
+__device__ __noinline__ float exact_e(float a, float v) {
+    const DeviceLib lib;
+    PllCtx c{};
+    float sv, cv;
+    if (!sincos_ctx_f(a, &sv, &cv, &c)) lib.sincosf_(a, &sv, &cv);
+    const float eI = v * cv;
+    const float eQ = v * (-sv);
+    float e;
+    if (!rot_atan2_f(eQ, eI, c, &e)) e = lib.atan2f_(eQ, eI);
+    return e;
+}
 
 // One wave a SIMD (amdgpu_waves_per_eu): the register budget is the chain's, so the scheduler
 // keeps each burst of reads whole instead of threading it through the steps for occupancy.
+// io / out: the stream's input and trigArg rows from the range's first sample (stride / ostride
+// floats a stream), n samples; st: the state (read at the start, the exact end state written).
 template <int NB, int BPI, int RD, int NC>
 __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))) pll_pipe_kernel(const float* io, int n, int n_streams, size_t stride,
-                                                      const double* side, size_t seg, double step, float norm_bw,
-                                                      const float* st, float* out_base, size_t ostride, int* fail,
-                                                      float2* rec, size_t rb, int inject, int miss) {
+                                                      double step, float norm_bw, float* st, float* out_base,
+                                                      size_t ostride, int inject, int miss,
+                                                      unsigned long long* stats) {
     constexpr int NI = NB * BPI;
     static_assert(NI == 16 || NI == 32 || NI == 64, "the evaluators' lane map: 64 / NI lanes a step");
     static_assert(NC == 3 || NC == 5, "three or five candidates");
@@ -523,13 +584,15 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     // rings of four intervals (interval k in slot k & 3; interval 0 is batch 0), per step: NC = 3:
     // the thresholds of c0 and c0 + 1 ulp and the e of c0 - 1 and c0 (sel), the e of c0 + 1
     // (sep); NC = 5: the thresholds of c0 - 1 .. c0 + 2 (sel), the e of c0 - 2 .. c0 + 1 (sel2),
-    // of c0 + 2 (sep); bits(c0) - HC (scb), P (spr); the chain's (integ, phase) at the end of each
-    // batch (sst); per interval the check's verdict (smiss) and "redone exactly" (sexact)
+    // of c0 + 2 (sep); bits(c0) - HC (scb), P (spr); the certification of each candidate's e
+    // (scert, byte r for c0 - HC + r); the chain's (integ, phase) at the end of each batch (sst);
+    // per interval the check's verdict (smiss) and "redone exactly" (sexact)
     __shared__ float4 sel[4][NI];
     __shared__ float4 sel2[NC == 5 ? 4 : 1][NC == 5 ? NI : 1];
     __shared__ float sep[4][NI];
     __shared__ uint32_t scb[4][NI];
     __shared__ double spr[4][NI];
+    __shared__ uint8_t scert[4][NI][8];
     __shared__ float2 sst[4][BPI];
     // one batch an interval (the 16-step form): the replay below would be as long as the chain's
     // own interval, so the chain hands over every phase instead (sph) and wave 2 checks those
@@ -541,7 +604,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     const int s = blockIdx.x;  // grid = n_streams
     const float* x = io + (size_t)s * stride;
     float* out = out_base + (size_t)s * ostride;
-    const float* S = st + 8 * (size_t)s;
+    float* S = st + 8 * (size_t)s;
     const float Kp = norm_bw * static_cast<float>(2.666);
     const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
     // the stream's state, uniform over the group (readfirstlane): the domain test below and every
@@ -550,59 +613,72 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     PllState p{uni(S[0]), uni(S[1]), uni(S[2]), uni(S[3]), uni(S[5])};
     // the variant's domain (uniform over the group): NC = 3 from 2^22; NC = 5 with 64-step
     // intervals in [2^21, 2^22), with 16-step ones in [2^20, 2^21)
-    if (!(NC == 3 ? pll_pipe_stream(p.trig, step, kPllPipeMin)
-                  : NI == 64 ? pll_pipe_stream(p.trig, step, kPllPipeMin5, kPllPipeMin - 1.0f)
-                             : pll_pipe_stream(p.trig, step, kPllPipeMinLow, kPllPipeMin5 - 1.0f)))
-        return;
+    const bool in_domain = NC == 3 ? pll_pipe_stream(p.trig, step, kPllPipeMin)
+                                   : NI == 64 ? pll_pipe_stream(p.trig, step, kPllPipeMin5, kPllPipeMin - 1.0f)
+                                              : pll_pipe_stream(p.trig, step, kPllPipeMinLow, kPllPipeMin5 - 1.0f);
     const float trig0 = p.trig;
+    const double t0d = (double)trig0;
+    // pll_side's P of step j (trigOffset after the step's increment, stuck at 2^24)
+    auto pr_at = [&](long long j) {
+        return step * (double)(float)fmin(t0d + (double)(j + 1), (double)kPllTrigStick);
+    };
     const int nb = n / NB;
-    const int ni = (nb - 1) / BPI;  // intervals after batch 0
-    const int inj = inject >= 0 && nb > 1 ? 1 + (inject + s) % (nb - 1) : -1;  // test hook: a wrong batch
-    // batches [k0, k1) exactly from state p (ctx): outputs, records, the test hook
-    auto exact = [&](PllState& q, PllCtx& c, int k0, int k1) {
-        for (int k = k0; k < k1; k++) {
-            const PllPair z = pll_redo(q, c, x + k * NB, out + k * NB, NB, Ki, Kp, step, true);
+    const int ni = nb > 0 ? (nb - 1) / BPI : 0;  // intervals after batch 0
+    // test hook: a miss on interval 1 + (inject + s) % ni of this stream (the exact redo runs)
+    const int inj = inject >= 0 && ni > 0 ? 1 + (inject + s) % ni : -1;
+    // steps [j0, j1) exactly from state q (c): outputs
+    auto exact = [&](PllState& q, PllCtx& c, long long j0, long long j1) {
+        if (j1 > j0) {
+            const PllPair z = pll_redo(q, c, x + j0, out + j0, (int)(j1 - j0), Ki, Kp, step, true);
             q = z.p;
             c = z.ctx;
-            if (k == inj) q.phase += 1.0e-3f;
-            if (t == 0) rec[(size_t)s * rb + k] = make_float2(q.integ, q.phase);
         }
     };
-    if (ni < 2) {  // a short segment: every batch exactly (no barrier is reached)
+    // a short range, or a stream outside the form's domain (the host's trigOffset bounds were
+    // wrong: costs speed, never bits): every step exactly (no barrier is reached)
+    if (ni < 2 || !in_domain) {
         if (w == 0) {
-            if (t == 0) fail[s] = nb;
             PllCtx c{};
             c.valid = false;
-            exact(p, c, 0, nb);
+            exact(p, c, 0, n);
+            if (t == 0) {
+                S[0] = p.integ; S[1] = p.phase; S[2] = p.fbI; S[3] = p.fbQ; S[5] = p.trig;
+                if (stats) {  // outside the domain: the whole range "resumed" on the exact path
+                    if (!in_domain) atomicAdd(stats, (unsigned long long)nb);
+                    atomicAdd(stats + 1, (unsigned long long)nb);
+                }
+            }
         }
         return;
     }
-    const double* ivs = side + (size_t)s * seg;
-    const double* prs = side + seg * (size_t)n_streams + (size_t)s * seg;
     auto j0 = [](int k) { return NB + (k - 1) * NI; };  // interval k's first step (k >= 1)
 
     if (w > 0) {
-        // ring of RD intervals of step data, interval k in slot k % RD, loaded RD - 1 ahead
+        // ring of RD intervals of step inputs, interval k in slot k % RD, loaded RD - 1 ahead
         float vq[RD];
-        double ivq[RD], prq[RD];
-        auto ld = [&](int k, float& v, double& iv, double& pr) {
+        auto ld = [&](int k, float& v) {
             const int j = j0(k <= ni ? k : ni) + l;
-            const int jn = min(j + 1, n - 1);  // the step the e is for
-            v = x[jn];
-            iv = ivs[jn];
-            pr = prs[j];
+            v = x[min(j + 1, n - 1)];  // the step the e is for
         };
         // interval k's candidate data from phase_ref, the phase at the start of interval k - 1:
-        // E1 lane (h, l) the e of candidates c0 - HC + r of step l, r = h, h + LPS, ... < NC; E2
-        // lane (h, l) the thresholds of c0 - HC + 1 + r, r = h, h + LPS, ... < NC - 1, lanes h = 0
-        // also c0's bits and P
-        auto put = [&](int k, float phase_ref, float v, double iv, double pr) {
+        // E1 lane (h, l) the e (and its certification) of candidates c0 - HC + r of step l, r = h,
+        // h + LPS, ... < NC; E2 lane (h, l) the thresholds of c0 - HC + 1 + r, r = h, h + LPS,
+        // ... < NC - 1, lanes h = 0 also c0's bits and P
+        auto put = [&](int k, float phase_ref, float v) {
+            const int j = j0(k <= ni ? k : ni) + l;
+            const double pr = pr_at(j);
             const float c0 = (float)(pr + (double)phase_ref);
             const uint32_t cb = __builtin_bit_cast(uint32_t, c0);
             const int sl = k & 3;
             if (w == 1) {
+                const double iv = pll_iv(v);
+                // one candidate at a time (unrolled, the five certified evaluations interleave and
+                // spill the kernel's registers)
+#pragma unroll 1
                 for (int r = h; r < NC; r += LPS) {
-                    const float e = pred_e(__builtin_bit_cast(float, cb + (uint32_t)(r - HC)), v, iv);
+                    bool ok;
+                    const float e = pred_e_cert(__builtin_bit_cast(float, cb + (uint32_t)(r - HC)), v, iv, ok);
+                    scert[sl][l][r] = ok ? 1 : 0;
                     if (r == NC - 1) sep[sl][l] = e;
                     else if (NC == 3) reinterpret_cast<float*>(&sel[sl][l])[2 + r] = e;
                     else reinterpret_cast<float*>(&sel2[NC == 5 ? sl : 0][NC == 5 ? l : 0])[r] = e;
@@ -619,10 +695,21 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         // E2: interval k's check.  Lane group g = t / NB replays batch g of the interval (BPI
         // batches) from the chain's state before it -- the chain's steps on the same candidate data,
         // so the same phases -- forms each step's trigArg float(P + phase) (filter.cpp:165) and
-        // checks it against the step's candidates; lane l of the group stores step l's.  A
-        // candidate that is not a positive finite float or a threshold outside its window (-inf)
-        // counts as a miss.  (The chain hands over one state a batch instead of every phase: an
-        // LDS store of four phases cost it ~20 cycles.)
+        // checks it against the step's candidates and that candidate's certification; lane l of
+        // the group stores step l's.  A candidate that is not a positive finite float, a
+        // threshold outside its window (-inf), an uncertified e or a state out of pll_batch_fast's
+        // range counts as a miss.  (The chain hands over one state a batch instead of every phase:
+        // an LDS store of four phases cost it ~20 cycles.)
+        auto verdict = [&](int sl, int J, float a) {
+            const uint32_t cm = scb[sl][J];
+            const float4 tt = sel[sl][J];
+            const float c0 = __builtin_bit_cast(float, cm + (uint32_t)HC);
+            const bool thr_ok = tt.x > -__builtin_inff() && tt.y > -__builtin_inff() &&
+                                (NC == 3 || (tt.z > -__builtin_inff() && tt.w > -__builtin_inff()));
+            const uint32_t idx = __builtin_bit_cast(uint32_t, a) - cm;
+            const bool cert = idx < (uint32_t)NC && scert[sl][J][idx < (uint32_t)NC ? idx : 0] != 0;
+            return !cert || !thr_ok || !(c0 > 0.0f && c0 < 3.0e38f);
+        };
         auto check = [&](int k) {
             if (w != 2) return;
             const int sl = k & 3;
@@ -631,18 +718,15 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 return;
             }
             if constexpr (!REPLAY) {  // the chain's phases, lanes h = 0
-                const float a = (float)(spr[sl][l] + (double)sph[REPLAY ? 0 : sl][REPLAY ? 0 : l]);
+                const float ph = sph[REPLAY ? 0 : sl][REPLAY ? 0 : l];
+                const float a = (float)(spr[sl][l] + (double)ph);
                 if (h == 0) out[j0(k) + l] = a;
-                const uint32_t cm = scb[sl][l];
-                const float4 tt = sel[sl][l];
-                const float c0 = __builtin_bit_cast(float, cm + (uint32_t)HC);
-                const bool thr_ok = tt.x > -__builtin_inff() && tt.y > -__builtin_inff() &&
-                                    (NC == 3 || (tt.z > -__builtin_inff() && tt.w > -__builtin_inff()));
-                const bool bad = (__builtin_bit_cast(uint32_t, a) - cm > (uint32_t)(NC - 1)) || !thr_ok ||
-                                 !(c0 > 0.0f && c0 < 3.0e38f);
-                bool any = __builtin_amdgcn_ballot_w64(h == 0 && bad) != 0;
-                if (k == min(miss, ni)) any = true;  // test hook: a miss on interval `miss` (the redo path)
-                if (t == 0) smiss[sl] = any ? 1 : 0;
+                // pll_batch_fast's range test, on the state at the batch's start
+                const float2 r0 = sst[(k - 1) & 3][BPI - 1];
+                const bool bad = verdict(sl, l, a) || !(fabsf(r0.y) < kPllMaxPhase && fabsf(r0.x) < kPllMaxInteg);
+                const bool any = __builtin_amdgcn_ballot_w64(h == 0 && bad) != 0 || k == min(miss, ni);
+                // test hooks: a forced miss (the redo path); inject's is counted as resumed
+                if (t == 0) smiss[sl] = k == inj ? 2 : any ? 1 : 0;
                 return;
             }
             const int g = t / NB, lg = t & (NB - 1);
@@ -651,7 +735,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             const float2 r0 = gb > 0 ? sst[sl][gb - 1] : sst[(k - 1) & 3][BPI - 1];
             float ig = r0.x, ph = r0.y;
             // step 0's candidate data: those of the trigArg before it (after an exactly redone
-            // interval that trigArg's e in every slot, as the chain's carry)
+            // interval that trigArg's exact e in every slot, as the chain's carry)
             float4 ca, ca2;
             float cep;
             if (gb > 0) {
@@ -659,8 +743,8 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 cep = sep[sl][NB * gb - 1];
                 ca2 = sel2[NC == 5 ? sl : 0][NC == 5 ? NB * gb - 1 : 0];
             } else if (sexact[(k - 1) & 3]) {
-                const int j = min(j0(k), n - 1);
-                const float e = pred_e((float)(prs[j0(k) - 1] + (double)ph), x[j], ivs[j]);
+                const int j = j0(k);
+                const float e = exact_e((float)(pr_at(j - 1) + (double)ph), x[min(j, n - 1)]);
                 ca = NC == 3 ? make_float4(0.0f, 0.0f, e, e) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                 ca2 = make_float4(e, e, e, e);
                 cep = e;
@@ -679,6 +763,8 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 dep[j] = sep[sl][NB * gb + j];
                 if constexpr (NC == 5) da2[j] = sel2[NC == 5 ? sl : 0][NC == 5 ? NB * gb + j : 0];
             }
+            // pll_batch_fast's range test, on the state at the batch's start
+            const bool range_ok = fabsf(r0.y) < kPllMaxPhase && fabsf(r0.x) < kPllMaxInteg;
             float mine = 0.0f;
 #pragma unroll
             for (int j = 0; j < NB; j++) {
@@ -692,22 +778,16 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             }
             const int J = NB * gb + lg;  // this lane's step
             const float a = (float)(spr[sl][J] + (double)mine);
-            const uint32_t cm = scb[sl][J];
-            const float4 tt = sel[sl][J];
-            const float c0 = __builtin_bit_cast(float, cm + (uint32_t)HC);
-            const bool thr_ok = tt.x > -__builtin_inff() && tt.y > -__builtin_inff() &&
-                                (NC == 3 || (tt.z > -__builtin_inff() && tt.w > -__builtin_inff()));
-            const bool bad = (__builtin_bit_cast(uint32_t, a) - cm > (uint32_t)(NC - 1)) || !thr_ok ||
-                             !(c0 > 0.0f && c0 < 3.0e38f);
+            const bool bad = verdict(sl, J, a) || !range_ok;
             if (act) out[j0(k) + J] = a;
-            bool any = __builtin_amdgcn_ballot_w64(act && bad) != 0;
-            if (k == min(miss, ni)) any = true;  // test hook: a miss on interval `miss` (the redo path)
-            if (t == 0) smiss[sl] = any ? 1 : 0;
+            const bool any = __builtin_amdgcn_ballot_w64(act && bad) != 0 || k == min(miss, ni);
+            // test hooks: a forced miss (the redo path); inject's is counted as resumed
+            if (t == 0) smiss[sl] = k == inj ? 2 : any ? 1 : 0;
         };
 #pragma unroll
-        for (int u = 0; u < RD; u++) ld(1 + u, vq[(1 + u) % RD], ivq[(1 + u) % RD], prq[(1 + u) % RD]);
-        put(1, p.phase, vq[1 % RD], ivq[1 % RD], prq[1 % RD]);  // interval 1 from the initial phase
-        ld(1 + RD, vq[1 % RD], ivq[1 % RD], prq[1 % RD]);
+        for (int u = 0; u < RD; u++) ld(1 + u, vq[(1 + u) % RD]);
+        put(1, p.phase, vq[1 % RD]);  // interval 1 from the initial phase
+        ld(1 + RD, vq[1 % RD]);
         __syncthreads();  // (prologue)
         unsigned long long ev_body = 0, ev_wait = 0;
         // interval i: interval i + 1's data, interval i - 1's check; groups of RD intervals from
@@ -721,8 +801,8 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                     if (i <= ni) {
                         const unsigned long long p0 = PROF_T();
                         if (i + 1 <= ni) {
-                            put(i + 1, sst[(i - 1) & 3][BPI - 1].y, vq[sl], ivq[sl], prq[sl]);
-                            ld(i + 1 + RD, vq[sl], ivq[sl], prq[sl]);
+                            put(i + 1, sst[(i - 1) & 3][BPI - 1].y, vq[sl]);
+                            ld(i + 1 + RD, vq[sl]);
                         }
                         check(i - 1);
                         const int redo = __builtin_amdgcn_readfirstlane(smiss[(i - 2) & 3]);
@@ -731,9 +811,8 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                             __syncthreads();
                             if (i + 1 <= ni) {  // interval i + 1 again, from the corrected phase
                                 float v;
-                                double iv, pr;
-                                ld(i + 1, v, iv, pr);
-                                put(i + 1, sst[(i - 1) & 3][BPI - 1].y, v, iv, pr);
+                                ld(i + 1, v);
+                                put(i + 1, sst[(i - 1) & 3][BPI - 1].y, v);
                             }
                         }
                         const unsigned long long p1 = PROF_T();
@@ -758,21 +837,19 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
 
     // ---- the chain
-    if (t == 0) fail[s] = nb;
     PllCtx ctx{};
     ctx.valid = false;
-    exact(p, ctx, 0, 1);  // batch 0 on the exact path (see pll_spec_kernel)
+    exact(p, ctx, 0, NB);  // batch 0 on the exact path (see pll_spec_kernel)
     float integ = p.integ, phase = p.phase;
     // (Ki, Kp) as an SGPR pair for the chain's v_pk_mul_f32 (uniform: readfirstlane)
     const uint64_t kk = (uint64_t)__builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, Ki)) |
                         ((uint64_t)__builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, Kp)) << 32);
     // the carry: step 0's candidate data (those of the previous interval's last trigArg); after
-    // an exact stretch that trigArg's e itself in every slot
+    // an exact stretch that trigArg's exact e in every slot
     float4 carry, carry2;
     float carry_ep;
     auto carry_exact = [&](float a, int k) {
-        const int j = min(j0(k), n - 1);
-        const float e = pred_e(a, x[j], ivs[j]);
+        const float e = exact_e(a, x[min(j0(k), n - 1)]);
         carry = NC == 3 ? make_float4(0.0f, 0.0f, e, e) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         carry2 = make_float4(e, e, e, e);
         carry_ep = e;
@@ -787,15 +864,14 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         }
     }
     __syncthreads();  // (prologue)
-    unsigned long long ch_body = 0, ch_wait = 0, n_redo = 0;
+    unsigned long long ch_body = 0, ch_wait = 0, n_redo = 0, n_inj = 0;
     for (int i = 1; i <= ni; i++) {
         const unsigned long long p0 = PROF_T();
         const int is = i & 3;
         const int flag = smiss[(i - 2) & 3];  // the verdict on interval i - 2 (slot 3 is clear at i = 1)
-        const int kb = 1 + (i - 1) * BPI;         // the interval's first batch
         // in bursts of CH steps: the data, 1.25 CH (NC = 5: 2.25 CH) 16-byte reads at once in the
         // order the steps need them (spread over the steps they stall the chain more,
-        // tools/ubench_chain.hip), then the steps, then the batch records
+        // tools/ubench_chain.hip), then the steps, then the batch states
         float4 A[CH], A2[NC == 5 ? CH : 1];
         float EP[CH];
         unroll_ic(
@@ -836,12 +912,6 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                         if constexpr ((J + 3) % NB == NB - 1) brec[(J + 3) / NB] = make_float2(integ, phase);
                     },
                     std::make_integer_sequence<int, CH / 4>{});
-                if constexpr (H == NI / CH - 1) {
-                    if (inj >= kb && inj < kb + BPI) {  // test hook, at the interval's end
-                        phase += 1.0e-3f;
-                        brec[CH / NB - 1].y = phase;
-                    }
-                }
                 // Every read of the burst has landed by now (the steps used them), but the waitcnt
                 // pass cannot tell: after the stores' exec-masked branch it would wait for the
                 // stores too (lgkmcnt(0)) before the next burst's first use.  Waiting here is free.
@@ -850,39 +920,37 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 __builtin_amdgcn_sched_barrier(0);
                 __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
                 __builtin_amdgcn_sched_barrier(0);
-                if (t == 0) {
-                    if constexpr (!REPLAY) {
+                // every lane stores (the chain's values are uniform: the same LDS words, the same
+                // arithmetic), so no lane test on the chain -- its lane id was spilled to scratch
+                // and reloaded at every burst
+                if constexpr (!REPLAY) {
 #pragma unroll
-                        for (int q = 0; q < CH / 4; q++)
-                            reinterpret_cast<float4*>(&sph[REPLAY ? 0 : is][REPLAY ? 0 : H * CH])[q] =
-                                *reinterpret_cast<const float4*>(&PH[REPLAY ? 0 : 4 * q]);
-                    }
-#pragma unroll
-                    for (int q = 0; q < CH / NB; q++) {
-                        sst[is][H * (CH / NB) + q] = brec[q];
-                        rec[(size_t)s * rb + kb + H * (CH / NB) + q] = brec[q];
-                    }
+                    for (int q = 0; q < CH / 4; q++)
+                        reinterpret_cast<float4*>(&sph[REPLAY ? 0 : is][REPLAY ? 0 : H * CH])[q] =
+                            *reinterpret_cast<const float4*>(&PH[REPLAY ? 0 : 4 * q]);
                 }
+#pragma unroll
+                for (int q = 0; q < CH / NB; q++) sst[is][H * (CH / NB) + q] = brec[q];
                 carry = A[CH - 1];
                 if constexpr (NC == 5) carry2 = A2[CH - 1];
                 carry_ep = EP[CH - 1];
             },
             std::make_integer_sequence<int, NI / CH>{});
-        if (t == 0) sexact[is] = 0;
+        sexact[is] = 0;
         if (__builtin_amdgcn_readfirstlane(flag)) {
             n_redo++;
+            n_inj += flag == 2 ? 1 : 0;
             __syncthreads();  // E2's stores of interval i - 1 happen before the redo's
-            // intervals i - 2 (missed), i - 1 and i exactly, from the state recorded before
+            // intervals i - 2 (missed), i - 1 and i exactly, from the state at the start of i - 2
+            // (the end of interval i - 3 in the ring; interval 0 is batch 0, slot 0 holds its end)
             const int f = i - 2;
-            const int kf = 1 + (f - 1) * BPI;
-            const float2 r0 = rec[(size_t)s * rb + kf - 1];
-            const float a = (float)(prs[j0(f) - 1] + (double)r0.y);  // the trigArg before it
+            const float2 r0 = sst[(f - 1) & 3][BPI - 1];
+            const float a = (float)(pr_at(j0(f) - 1) + (double)r0.y);  // the trigArg before it
             PllState q;
             PllCtx c{};
             pll_state_at(q, c, r0.x, r0.y, trig0, (long long)j0(f), a, DeviceLib{});
             for (int k = f; k <= i; k++) {
-                const int k0 = 1 + (k - 1) * BPI;
-                exact(q, c, k0, k0 + BPI);
+                exact(q, c, j0(k), j0(k) + NI);
                 if (t == 0) {
                     sst[k & 3][BPI - 1] = make_float2(q.integ, q.phase);
                     if (k > f) sexact[k & 3] = 1;
@@ -900,17 +968,26 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         ch_wait += PROF_T() - p1;
     }
     __syncthreads();  // E2's checks of the last two intervals
-    // a miss in them: from the first missed interval on exactly; then the batches past the last
-    // interval exactly
+    // a miss in them: from the first missed interval on exactly; then the steps past the last
+    // interval exactly, from the state at the end of the last good interval
     const int f = smiss[(ni - 1) & 3] ? ni - 1 : (smiss[ni & 3] ? ni : ni + 1);
-    const int kf = 1 + (f - 1) * BPI;
-    const float2 r0 = f <= ni ? rec[(size_t)s * rb + kf - 1] : make_float2(integ, phase);
-    if (kf < nb) {
-        const float a = (float)(prs[j0(f) - 1] + (double)r0.y);
-        PllState q;
-        PllCtx c{};
-        pll_state_at(q, c, r0.x, r0.y, trig0, (long long)j0(f), a, DeviceLib{});
-        exact(q, c, kf, nb);
+    const float2 r0 = sst[(f - 1) & 3][BPI - 1];
+    const long long jf = j0(f);
+    const float a = (float)(pr_at(jf - 1) + (double)r0.y);
+    PllState q;
+    PllCtx c{};
+    pll_state_at(q, c, r0.x, r0.y, trig0, jf, a, DeviceLib{});
+    exact(q, c, jf, n);
+    if (t == 0) {
+        S[0] = q.integ; S[1] = q.phase; S[2] = q.fbI; S[3] = q.fbQ; S[5] = q.trig;
+        // fmrx_debug_pll_stats: batches run; "resumed" only for the inject hook's forced redos
+        // (the runner is exact by construction: its own redos of missed intervals are internal)
+        if (stats) {
+            int fin = 0;  // the verdicts read after the loop
+            for (int k = ni - 1; k <= ni; k++) fin += smiss[k & 3] == 2 ? 1 : 0;
+            atomicAdd(stats, (n_inj + (unsigned long long)fin) * 3 * BPI);
+            atomicAdd(stats + 1, (unsigned long long)nb);
+        }
     }
 #ifdef FMRX_AB_PROF
     if (t == 0) {
@@ -923,6 +1000,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     (void)ch_body;
     (void)ch_wait;
     (void)n_redo;
+    (void)n_inj;
 }
 
 }  // namespace
@@ -956,21 +1034,22 @@ void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_str
                        seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, sat_ok, pipe_on);
 }
 
-void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_t stride, const double* side,
-                     size_t seg, double step, float norm_bw, const float* st, float* out, size_t ostride, int* fail,
-                     float2* rec, size_t rb, int inject, int miss, bool from22, bool from21, bool from20) {
+void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
+                     float* st, float* out, size_t ostride, int inject, int miss, int form,
+                     unsigned long long* stats) {
 #ifdef FMRX_AB_PROF
     reg_pred_prof();
 #endif
-    if (from22)
+    if (n <= 0) return;
+    if (form == 22)
         hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8, 3>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
-                           stride, side, seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, miss);
-    if (from21)
+                           stride, step, norm_bw, st, out, ostride, inject, miss, stats);
+    else if (form == 21)
         hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
-                           stride, side, seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, miss);
-    if (from20)
+                           stride, step, norm_bw, st, out, ostride, inject, miss, stats);
+    else
         hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 1, 8, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
-                           stride, side, seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, miss);
+                           stride, step, norm_bw, st, out, ostride, inject, miss, stats);
 }
 
 }  // namespace fmrx

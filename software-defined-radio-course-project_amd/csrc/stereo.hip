@@ -134,9 +134,12 @@ __global__ void bpf_pair_generic(StereoLaunch L, BpTaps t) {
 // the stream-major input are read coalesced, the stream-minor pairs written coalesced.
 constexpr int kPrepS = 16, kPrepJ = 64;
 __global__ void __launch_bounds__(256) pll_prep_kernel(const float* io, int m, int n_streams, size_t stride,
-                                                       double* side, size_t seg, const float* st, double step) {
+                                                       double* side, size_t seg, const float* st, double step,
+                                                       int* fail) {
     __shared__ double2 t_iv[kPrepJ / 2][kPrepS], t_pr[kPrepJ / 2][kPrepS], t_h[kPrepJ / 2][kPrepS];
     const int j0 = blockIdx.x * kPrepJ, s0 = blockIdx.y * kPrepS;
+    // fail[] sentinel: 0 (= resume the whole segment exactly) until a runner claims the stream
+    if (fail && blockIdx.x == 0 && threadIdx.x < kPrepS && s0 + (int)threadIdx.x < n_streams) fail[s0 + threadIdx.x] = 0;
     for (int e = threadIdx.x; e < kPrepS * kPrepJ; e += blockDim.x) {
         const int r = e / kPrepJ, c = e % kPrepJ, s = s0 + r, j = j0 + c;
         double iv = 0.0, pr = 0.0;
@@ -171,9 +174,13 @@ __global__ void __launch_bounds__(256) pll_prep_kernel(const float* io, int m, i
 // runner is not launched for the segment): 16 B a sample written instead of 32.
 __global__ void __launch_bounds__(256) pll_prep_major_kernel(const float* io, int m, int n_streams, size_t stride,
                                                              double* side, size_t seg, const float* st, double step,
-                                                             int with_h) {
+                                                             int with_h, int* fail) {
     const int s = blockIdx.y;
     const int jp = blockIdx.x * blockDim.x + threadIdx.x;
+    // fail[] sentinel: 0 = pll_kernel resumes the whole segment on the certified path.  Every
+    // runner that takes stream s overwrites it (fail[s] = nb, then the check's atomicMin), so a
+    // stream no launched runner took -- a wrong trigOffset hint -- costs speed, never bits.
+    if (fail && jp == 0) fail[s] = 0;
     if (2 * jp >= m) return;
     const float t0 = st[8 * (size_t)s + 5];
     double2 iv, pr, h;
@@ -875,36 +882,45 @@ int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s) {
     return ok();
 }
 
-// One segment's scratch, in doubles: the side data (iv, pr, half turns: 3 seg), the speculative runner's
-// trigArgs (seg floats), its batch records (seg / 16 float2) per stream, and fail[] (ints).
-// Segment length: kPllSeg samples up to 32 streams, then shorter so that segment x streams
-// stays ~2^23 (down to 2^14): a batch the runner got wrong (~3e-9 of steps) costs the rest
-// of its segment on the certified path, serially, so the expected cost per segment grows with
-// segment^2 x streams; launches per segment are ~4 (tens of microseconds).
+// The scratch of a launch_pll call, in doubles: one segment's side data (iv, pr, half turns:
+// 3 seg, plus seg as slack for the stream-minor layout), the call's trigArgs (n floats a stream:
+// every runner writes its steps' trigArgs there, the NCO reads them once at the end), the
+// speculative runners' batch records (seg / 16 float2 a stream) and fail[] (ints).
+// Segment length (the lane / two-wave / saturated runners, checked by pll_check_kernel): kPllSeg
+// samples up to 32 streams, then shorter so that segment x streams stays ~2^23 (down to 2^14): a
+// batch the runner got wrong (~3e-9 of steps) costs the rest of its segment on the certified
+// path, serially, so the expected cost per segment grows with segment^2 x streams.  The
+// three-wave runner certifies itself and needs no segments (pll_pipe_kernel).
 static size_t pll_seg_len(int n, int n_streams) {
     size_t cap = kPllSeg;
     while (cap > ((size_t)1 << 14) && cap * (size_t)std::max(n_streams, 1) > ((size_t)1 << 23)) cap >>= 1;
     return std::min<size_t>(((size_t)std::max(n, 0) + 15) / 16 * 16, cap);
 }
 size_t pll_side_doubles(int n, int n_streams) {
-    const size_t seg = pll_seg_len(n, n_streams);
-    return (4 * seg + seg / 2 + seg / kPllBatch) * (size_t)n_streams + ((size_t)n_streams + 1) / 2;
+    const size_t seg = pll_seg_len(n, n_streams), ns = (size_t)n_streams;
+    return 4 * seg * ns + ((size_t)std::max(n, 0) * ns + 1) / 2 + (seg / kPllBatch) * ns + (ns + 1) / 2;
 }
 
-// The recurrence in segments of at most kPllSeg samples per stream: side data of the segment
-// (parallel), then the serial PLL over it; the state carries in st between launches, so the
-// segments chain exactly like one launch.  Then the NCO of the segment's samples in parallel.
-// A segment runs speculatively (pll_spec_kernel, pll_check_kernel, then pll_kernel resuming at
-// the first batch that did not verify) unless FMRX_PLL_SPEC=0 or the streams' rows are not
-// 16-byte aligned; the plain path is pll_kernel in place.
+// The PLL over n samples of n_streams streams, then the NCO of every sample in parallel
+// (filter.cpp:136-174).  With the host's trigOffset bounds known and equal for every stream
+// (every context's streams advance together) and a SIMD for each of the three-wave runner's
+// waves, the samples from trigOffset 2^20 on run on it: one self-certifying launch per form
+// (pll_pipe_kernel; 2^20 / 2^21 / 2^22), no per-segment kernels.  The samples before, or all of
+// them otherwise, run in segments (pll_seg_len): side data of the segment (parallel), the
+// speculative runner (pll_spec_lane_kernel, pll_pred_kernel or pll_sat_kernel by regime,
+// pll_spec_kernel beyond 4 streams a wave), pll_check_kernel, then pll_kernel resuming at the
+// first batch that did not verify; the state carries in st between launches, so the segments
+// chain exactly like one launch.  FMRX_PLL_SPEC=0 (or rows not 16-byte aligned): the plain
+// certified pll_kernel in place.
 int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
                float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s,
                const PllHint& hint, unsigned long long* spec_stats) {
     if (n <= 0) return 0;
     const size_t seg = pll_seg_len(n, n_streams);
     const size_t rb = seg / kPllBatch;
-    float* args = reinterpret_cast<float*>(side + 4 * seg * (size_t)n_streams);  // seg per stream
-    float2* rec = reinterpret_cast<float2*>(args + seg * (size_t)n_streams);      // rb per stream
+    float* args = reinterpret_cast<float*>(side + 4 * seg * (size_t)n_streams);  // n per stream
+    float2* rec = reinterpret_cast<float2*>(side + 4 * seg * (size_t)n_streams +
+                                            ((size_t)n * n_streams + 1) / 2);  // rb per stream
     int* fail = reinterpret_cast<int*>(rec + rb * (size_t)n_streams);
     // one stream per wave while the waves fit one per SIMD, then more streams per wave
     const int n_simd = hint.n_simd;
@@ -912,8 +928,9 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         const char* e = std::getenv("FMRX_PLL_SPEC");
         return !(e && e[0] == '0');
     }();
-    // test hook (tests/test_gpu_parity.py): the runner corrupts batch 1 + (k + s) % (nb - 1) of
-    // stream s, so the check and the fix-up from that batch run on every stream
+    // test hook (tests/test_gpu_parity.py): the runners corrupt batch 1 + (k + s) % (nb - 1) of
+    // stream s (the three-wave runner: a forced miss on one interval), so the check and the
+    // fix-up from that batch (the exact redo) run on every stream
     const int inject = [] {
         const char* e = std::getenv("FMRX_PLL_SPEC_INJECT");
         return e ? std::atoi(e) : -1;
@@ -938,9 +955,8 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     const int wpg = waves > n_simd / 4 ? 4 : 1;
     const dim3 grid((waves + wpg - 1) / wpg), block(64 * wpg);
 
-    // filter.cpp:163: 2*PI*(freq/Fs) in double from the float quotient (host == device IEEE)
     // FMRX_PLL_PIPE=0 (measurements, tests): no three-wave runner; FMRX_PLL_PIPE_MISS=k (test
-    // hook): its check reports a miss on interval k of every segment, so the redo path runs
+    // hook): its check reports a miss on interval k of every launch, so the redo path runs
     const int pipe_env = [] {
         const char* e = std::getenv("FMRX_PLL_PIPE");
         return (e && e[0] == '0') ? 0 : 1;
@@ -949,78 +965,122 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         const char* e = std::getenv("FMRX_PLL_PIPE_MISS");
         return e ? std::atoi(e) : -1;
     }();
-
+    // FMRX_PLL_HINT_SKEW=d (test hook): the host's trigOffset bounds shifted by d samples, so the
+    // runners launched are the wrong ones.  A segment stream no runner takes keeps the pre-pass's
+    // fail[] sentinel 0 and is resumed whole on the certified path; a three-wave launch outside its
+    // domain runs its range exactly (same bits either way)
+    const double skew = [] {
+        const char* e = std::getenv("FMRX_PLL_HINT_SKEW");
+        return e ? std::atof(e) : 0.0;
+    }();
+    // filter.cpp:163: 2*PI*(freq/Fs) in double from the float quotient (host == device IEEE)
     const double step = (2.0 * 3.14159265358979323846) * static_cast<double>(freq / fs);  // dy4.h:14 PI
     const bool step_ok = std::fabs(step * (double)kPllTrigStick) < kPllMaxPr;
-    for (size_t off = 0; off < (size_t)n; off += seg) {
-        // the runners a segment can need (pll_pipe_stream / pll_sat_segment / pll_pred_wave take
-        // their streams, the lane kernel the rest): with known trigOffset bounds the others are
-        // not launched.  The three-wave runner wants a SIMD per wave: one stream a workgroup
-        const double lo = std::min(hint.trig_lo + (double)off, (double)kPllTrigStick);
-        const double hi = std::min(hint.trig_hi + (double)off, (double)kPllTrigStick);
-        const bool k = hint.known && step_ok;
-        // (3 x streams <= SIMDs implies the two-wave runner fits too, so the lane kernel, told to
-        // leave the predicted runners' streams, also leaves the three-wave runner's)
-        const bool run_pipe = spec && pred_ok && pipe_env && spw == 1 && 3 * n_streams <= n_simd &&
-                              (!k || hi >= (double)kPllPipeMinLow);
-        const bool pipe_all = run_pipe && k && lo >= (double)kPllPipeMinLow;  // every stream to it
-        const bool pipe22 = run_pipe && (!k || hi >= (double)kPllPipeMin);
-        const bool pipe21 = run_pipe && (!k || (lo < (double)kPllPipeMin && hi >= (double)kPllPipeMin5));
-        const bool pipe20 = run_pipe && (!k || lo < (double)kPllPipeMin5);
+    const double hlo = std::max(hint.trig_lo + skew, 0.0), hhi = std::max(hint.trig_hi + skew, 0.0);
+    const bool k = hint.known && step_ok;
+    StageTimer* tm = hint.timer;
+    auto timed = [&](int kind, double steps, auto&& launch) {
+        const int t = tm ? tm->begin(s) : -1;
+        launch();
+        if (tm) tm->end(t, kind, steps, s);
+    };
+    // the three-wave runner: every stream at the same known trigOffset t, a SIMD per wave (one
+    // stream a workgroup of three); it takes the samples from trigOffset 2^20 on
+    const bool pipe = spec && pred_ok && pipe_env && spw == 1 && 3 * n_streams <= n_simd && k && hlo == hhi;
+    size_t n_seg = (size_t)n;  // samples through the segment loop
+    if (pipe) n_seg = hlo >= (double)kPllPipeMinLow ? 0 : std::min((size_t)n, (size_t)((double)kPllPipeMinLow - hlo));
+
+    for (size_t off = 0; off < n_seg; off += seg) {
+        // the runners a segment can need (pll_sat_segment / pll_pred_wave take their streams, the
+        // lane kernel the rest): with known trigOffset bounds the others are not launched
+        const double lo = std::min(hlo + (double)off, (double)kPllTrigStick);
+        const double hi = std::min(hhi + (double)off, (double)kPllTrigStick);
         // the two-wave runner too wants a SIMD per wave (two of its waves on one SIMD ran slower
         // than the lane runner: 1,024 streams x 10 s 0.291 vs 0.279 s, 2,048 0.405 vs 0.371 s)
         const bool pred_fit = pred_ok && (2 * waves <= n_simd || pred_ok == 2);
-        const bool sat_all = k && sat_ok && spw == 1 && !run_pipe && lo >= (double)kPllTrigStick;
+        const bool sat_all = k && sat_ok && spw == 1 && lo >= (double)kPllTrigStick;
         const bool run_lane = !(k && lo >= (double)kPllPredMin && (pred_fit || sat_all));
-        const bool run_sat = sat_ok && spw == 1 && !run_pipe && (!k || hi >= (double)kPllTrigStick);
-        const bool run_pred = pred_fit && (!k || hi >= (double)kPllPredMin) && !sat_all && !pipe_all;
-        const int m = (int)std::min(seg, (size_t)n - off);
+        const bool run_sat = sat_ok && spw == 1 && (!k || hi >= (double)kPllTrigStick);
+        const bool run_pred = pred_fit && (!k || hi >= (double)kPllPredMin) && !sat_all;
+        const int m = (int)std::min(seg, n_seg - off);
         float* x = io + off;
-        if (spw <= 4)  // the split kernels read stream-major side data
-            hipLaunchKernelGGL(pll_prep_major_kernel, dim3(((m + 1) / 2 + 255) / 256, n_streams), dim3(256), 0, s, x, m,
-                               n_streams, stride, side, seg, st, step, (spec && run_lane) ? 1 : 0);
-        else
-            hipLaunchKernelGGL(pll_prep_kernel, dim3((m + kPrepJ - 1) / kPrepJ, (n_streams + kPrepS - 1) / kPrepS),
-                               dim3(256), 0, s, x, m, n_streams, stride, side, seg, st, step);
-        float* out = spec ? args : x;
-        const size_t ostride = spec ? seg : stride;
+        float* out = spec ? args + off : x;
+        const size_t ostride = spec ? (size_t)n : stride;
+        // a runner's steps count toward its regime only when it is the segment's one runner
+        const bool lane_on = spec && spw <= 4 && run_lane, sat_on = spec && spw <= 4 && run_sat,
+                   pred_on = spec && spw <= 4 && run_pred;
+        const double one = (int)lane_on + sat_on + pred_on == 1 ? (double)m : 0.0;
+        timed(kStPrep, 0.0, [&] {
+            if (spw <= 4)  // the split kernels read stream-major side data
+                hipLaunchKernelGGL(pll_prep_major_kernel, dim3(((m + 1) / 2 + 255) / 256, n_streams), dim3(256), 0, s,
+                                   x, m, n_streams, stride, side, seg, st, step, (spec && run_lane) ? 1 : 0,
+                                   spec ? fail : nullptr);
+            else
+                hipLaunchKernelGGL(pll_prep_kernel, dim3((m + kPrepJ - 1) / kPrepJ, (n_streams + kPrepS - 1) / kPrepS),
+                                   dim3(256), 0, s, x, m, n_streams, stride, side, seg, st, step, spec ? fail : nullptr);
+        });
         if (spec) {
             if (spw <= 4) {
                 if (run_lane)
-                    hipLaunchKernelGGL(pll_spec_lane_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw,
-                                       stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject,
-                                       run_sat ? 1 : 0, run_pred ? 1 : 0);  // it leaves waves only to those launched
+                    timed(kStLane, one, [&] {
+                        hipLaunchKernelGGL(pll_spec_lane_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw,
+                                           stride, side, seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject,
+                                           run_sat ? 1 : 0, run_pred ? 1 : 0);  // it leaves waves only to those launched
+                    });
                 // saturated streams (pll_sat_segment), which the lane kernel leaves to it
                 if (run_sat)
-                    launch_pll_sat(grid, block, s, x, m, n_streams, spw, stride, side, seg, step, norm_bw, st, args,
-                                   seg, fail, rec, rb, inject);
+                    timed(kStSat, one, [&] {
+                        launch_pll_sat(grid, block, s, x, m, n_streams, spw, stride, side, seg, step, norm_bw, st,
+                                       out, ostride, fail, rec, rb, inject);
+                    });
                 // waves from trigOffset 2^20 below the stick (pll_pred_wave)
                 if (run_pred)
-                    launch_pll_pred(waves, s, x, m, n_streams, spw, stride, side, seg, step, norm_bw, st, args, seg,
-                                    fail, rec, rb, inject, run_sat ? 1 : 0, run_pipe ? 1 : 0);
-                // one stream a workgroup from trigOffset 2^20 (pll_pipe_stream)
-                if (run_pipe)
-                    launch_pll_pipe(s, x, m, n_streams, stride, side, seg, step, norm_bw, st, args, seg, fail, rec,
-                                    rb, inject, pipe_miss, pipe22, pipe21, pipe20);
+                    timed(kStPred, one, [&] {
+                        launch_pll_pred(waves, s, x, m, n_streams, spw, stride, side, seg, step, norm_bw, st, out,
+                                        ostride, fail, rec, rb, inject, run_sat ? 1 : 0, 0);
+                    });
             } else
-                hipLaunchKernelGGL(pll_spec_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw,
-                                   stride, side, seg, step, norm_bw, st, args, seg, fail, rec, rb, inject);
+                timed(kStLane, (double)m, [&] {
+                    hipLaunchKernelGGL(pll_spec_kernel<kPllBatch>, grid, block, 0, s, x, m, n_streams, spw, stride,
+                                       side, seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject);
+                });
             const int nb = m / kPllBatch;
             if (nb > 0)
-                hipLaunchKernelGGL(pll_check_kernel<kPllBatch>, dim3((nb + 63) / 64, n_streams), dim3(64), 0, s, x, m,
-                                   stride, step, norm_bw, st, args, seg, fail, rec, rb);
+                timed(kStCheck, 0.0, [&] {
+                    hipLaunchKernelGGL(pll_check_kernel<kPllBatch>, dim3((nb + 63) / 64, n_streams), dim3(64), 0, s, x,
+                                       m, stride, step, norm_bw, st, out, ostride, fail, rec, rb);
+                });
         }
-        if (spw <= 4)
-            hipLaunchKernelGGL((pll_kernel<kPllBatch, true>), grid, block, 0, s, x, m, n_streams, spw, stride,
-                               side, seg, step, norm_bw, st, out, ostride, spec ? fail : nullptr, rec, rb,
-                               spec_stats);
-        else
-            hipLaunchKernelGGL((pll_kernel<kPllBatch, false>), grid, block, 0, s, x, m, n_streams, spw, stride,
-                               side, seg, step, norm_bw, st, out, ostride, spec ? fail : nullptr, rec, rb,
-                               spec_stats);
-        hipLaunchKernelGGL(pll_nco_kernel, dim3((m + 255) / 256, n_streams), dim3(256), 0, s, x, m, stride, out,
-                           ostride, nco_scale, phase_adjust, st);
+        timed(kStTail, 0.0, [&] {
+            if (spw <= 4)
+                hipLaunchKernelGGL((pll_kernel<kPllBatch, true>), grid, block, 0, s, x, m, n_streams, spw, stride,
+                                   side, seg, step, norm_bw, st, out, ostride, spec ? fail : nullptr, rec, rb,
+                                   spec_stats);
+            else
+                hipLaunchKernelGGL((pll_kernel<kPllBatch, false>), grid, block, 0, s, x, m, n_streams, spw, stride,
+                                   side, seg, step, norm_bw, st, out, ostride, spec ? fail : nullptr, rec, rb,
+                                   spec_stats);
+        });
     }
+    // the three-wave runner's ranges: [2^20, 2^21) 16-step five-candidate form, [2^21, 2^22) the
+    // 64-step one, from 2^22 (the stick included) three candidates
+    for (size_t j = n_seg; pipe && j < (size_t)n;) {
+        const double t = std::min(hlo + (double)j, (double)kPllTrigStick);
+        const int form = t < (double)kPllPipeMin5 ? 20 : t < (double)kPllPipeMin ? 21 : 22;
+        const size_t end = form == 20 ? (size_t)((double)kPllPipeMin5 - hlo)
+                         : form == 21 ? (size_t)((double)kPllPipeMin - hlo) : (size_t)n;
+        const size_t e = std::min(end, (size_t)n);
+        timed(form == 20 ? kStPipe20 : form == 21 ? kStPipe21 : kStPipe22, (double)(e - j), [&] {
+            launch_pll_pipe(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j, (size_t)n, inject,
+                            pipe_miss, form, spec_stats);
+        });
+        j = e;
+    }
+    // the NCO of every sample from its trigArg (filter.cpp:170), in parallel, over the input in place
+    timed(kStNco, 0.0, [&] {
+        hipLaunchKernelGGL(pll_nco_kernel, dim3((n + 255) / 256, n_streams), dim3(256), 0, s, io, n, stride,
+                           spec ? args : io, spec ? (size_t)n : stride, nco_scale, phase_adjust, st);
+    });
     return ok();
 }
 

@@ -85,76 +85,181 @@ def fmrx_process_fn(fmrx, mode: int, channels: int, n_blocks: int, device: int, 
     return process
 
 
+def _flag_device(pg: bool, device):
+    """Where a collective's small tensors live: the GPU for RCCL, host memory for gloo."""
+    return device if pg and dist.get_backend() == "nccl" else "cpu"
+
+
+def all_ok(ok: bool, pg: bool, device=None) -> bool:
+    """Every rank learns whether EVERY rank succeeded so far (MAX over ranks of an error flag).
+    A rank that failed before a collective must not leave the others blocked in it: each rank
+    calls this at the same points, and all of them skip the collectives together when any failed."""
+    if not pg:
+        return ok
+    t = torch.tensor([0 if ok else 1], dtype=torch.int32, device=_flag_device(pg, device))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.item()) == 0
+
+
+def per_rank(values: Sequence[float], pg: bool, device=None) -> list[list[float]]:
+    """Every rank's `values` (same length on every rank), in rank order, on every rank."""
+    t = torch.tensor(list(values), dtype=torch.float64, device=_flag_device(pg, device))
+    if not pg:
+        return [t.tolist()]
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [p.tolist() for p in parts]
+
+
+def run_leg(setup: Callable[[], object], process: Callable[[object], torch.Tensor], n_streams: int, pcm_len: int,
+            world: int, rank: int, pg: bool, device=None, cleanup: Callable[[object], None] | None = None,
+            post: Callable[[object], dict] | None = None) -> dict:
+    """One timed multi-stream step with failure agreement (the collective skeleton of
+    streams_leg, also run on the CPU with gloo by the tests).
+
+    setup() prepares this rank's shard (untimed; may raise); process(state) -> [n_local, pcm_len]
+    PCM is the timed step (may raise).  Timing = barrier -> process -> gather to rank 0.  Before
+    the barrier and again before the gather every rank agrees on success (all_ok), so a rank
+    that raised does not leave the others in a collective.  Returns a dict on every rank:
+    `error` when any rank failed, else per-rank seconds (total, process, gather) and, on rank 0,
+    `gathered` ([n_streams, pcm_len])."""
+    import time
+
+    err, state = None, None
+    try:
+        state = setup()
+    except Exception as e:  # noqa: BLE001 -- reported, and every rank skips the collectives
+        err = f"rank {rank} setup: {e!r}"
+    try:
+        if not all_ok(err is None, pg, device):
+            return {"error": err or "another rank failed in setup; collectives skipped"}
+        if pg:
+            dist.barrier()
+        if device is not None and torch.cuda.is_available():
+            torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        local = None
+        try:
+            local = process(state)
+            assert local.shape[1:] == (pcm_len,), (tuple(local.shape), pcm_len)
+        except Exception as e:  # noqa: BLE001
+            err = f"rank {rank} process: {e!r}"
+        t1 = time.perf_counter()
+        if not all_ok(err is None, pg, device):
+            return {"error": err or "another rank failed in the timed step; gather skipped"}
+        gathered = gather_pcm(local, n_streams, pcm_len, world, rank) if pg else local
+        if device is not None and torch.cuda.is_available():
+            torch.cuda.synchronize(device)
+        t2 = time.perf_counter()
+        ranks = per_rank([t2 - t0, t1 - t0, t2 - t1], pg, device)
+        res = {"per_rank": ranks, "total": max(r[0] for r in ranks), "process": max(r[1] for r in ranks),
+               "gather": max(r[2] for r in ranks)}
+        if rank == 0:
+            res["gathered"] = gathered
+            if post is not None:  # after the timed step, untimed (rank 0's shard only)
+                try:
+                    res["post"] = post(state)
+                except Exception as e:  # noqa: BLE001 -- diagnostic only
+                    res["post"] = {"error": repr(e)}
+        return res
+    finally:
+        if cleanup is not None and state is not None:
+            cleanup(state)
+
+
 def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, device: int,
                 mode: int = 0, expect: dict | None = None, warmup: bool = True,
-                collective: bool | None = None) -> dict | None:
+                collective: bool | None = None, profile: Callable | None = None) -> dict | None:
     """BASELINE configs[4] as one timed step: `n_streams` independent stereo streams (stream id
     = synth seed) of `seconds` each, this rank's contiguous shard processed as ONE multi-stream
     device-resident call, then the S16 PCM gathered to rank 0 (RCCL over xGMI; gloo rehearses
-    it).  Timing = barrier -> process -> gather, max over ranks.  The input is synthesized on the
-    device in one launch before the timed region; `warmup` runs one untimed full-size call first
-    (code objects, scratch sized) and restarts from the power-on state.  `expect` maps stream id
-    -> the reference build's PCM SHA-256 (tests/golden/hashes.json streams_*); rank 0 checks
-    those streams of the gathered PCM.  `collective` (default: world > 1) routes the barrier,
-    gather and timing reduction through the initialised process group; without it (one rank, no
-    process group) the rank's PCM is the result.  Returns rank 0's result dict (None elsewhere)."""
+    it).  Timing = barrier -> process -> gather, max over ranks, with every rank's own split
+    (`per_rank`: seconds, seconds_process, seconds_gather) so a multi-GPU run shows which rank
+    or which phase is slow.  The input is synthesized on the device in one launch before the
+    timed region; `warmup` runs one untimed full-size call first (code objects, scratch sized)
+    and restarts from the power-on state.  `expect` maps stream id -> the reference build's PCM
+    SHA-256 (tests/golden/hashes.json streams_*); rank 0 checks those streams of the gathered
+    PCM (`parity` says "unpinned" when none are recorded for this length).  `collective`
+    (default: world > 1) routes the barrier, gather and timing reduction through the process
+    group; without it (one rank, no process group) the rank's PCM is the result.  A failure on
+    any rank is agreed on before each collective (run_leg), so no rank hangs in one.  Returns
+    rank 0's result dict (None elsewhere)."""
     import hashlib
     import time
 
     ids = list(shard(n_streams, world, rank))
-    rx = fmrx.Receiver(mode, fmrx.STEREO, n_streams=max(1, len(ids)), device=device)
-    try:
-        bb = rx.geo.block_bytes
-        nb = int(seconds * rx.geo.rf_fs * 2 // bb)
-        pcm_len = nb * rx.geo.pcm_samples
-        dev = torch.device("cuda", device)
-        iq = torch.empty((max(1, len(ids)), nb * bb), dtype=torch.uint8, device=dev)
-        out = torch.empty((len(ids), pcm_len), dtype=torch.int16, device=dev)
-        torch.cuda.synchronize(dev)
-        t_synth = time.perf_counter()
+    pg = world > 1 if collective is None else collective
+    dev = torch.device("cuda", device)
+    geo = fmrx.geometry(fmrx.default_config(mode, fmrx.STEREO))
+    bb = geo.block_bytes
+    nb = int(seconds * geo.rf_fs * 2 // bb)
+    pcm_len = nb * geo.pcm_samples
+    t_synth = [0.0]
+
+    def setup():
+        rx = fmrx.Receiver(mode, fmrx.STEREO, n_streams=max(1, len(ids)), device=device)
+        try:
+            iq = torch.empty((max(1, len(ids)), nb * bb), dtype=torch.uint8, device=dev)
+            out = torch.empty((len(ids), pcm_len), dtype=torch.int16, device=dev)
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            if ids:
+                rx.synth_device_streams(ids, 0, nb * bb // 2, iq.data_ptr(), nb * bb)
+                rx.synchronize()
+            t_synth[0] = time.perf_counter() - t
+            if ids and warmup:
+                rx.process_device(iq.data_ptr(), nb, out.data_ptr())
+                rx.synchronize()
+                rx.reset()
+        except Exception:
+            rx.close()
+            raise
+        return rx, iq, out
+
+    def process(state):
+        rx, iq, out = state
         if ids:
-            rx.synth_device_streams(ids, 0, nb * bb // 2, iq.data_ptr(), nb * bb)
-        t_synth = time.perf_counter() - t_synth
-        if ids and warmup:
             rx.process_device(iq.data_ptr(), nb, out.data_ptr())
             rx.synchronize()
-            rx.reset()
-        pg = world > 1 if collective is None else collective
-        if pg:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        if ids:
-            rx.process_device(iq.data_ptr(), nb, out.data_ptr())
-            rx.synchronize()
-        t1 = time.perf_counter()
-        gathered = gather_pcm(out, n_streams, pcm_len, world, rank) if pg else out
-        torch.cuda.synchronize(dev)
-        t2 = time.perf_counter()
-        t = torch.tensor([t2 - t0, t1 - t0, t2 - t1],
-                         device=dev if pg and dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
-        if pg:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        total, proc, gat = (float(v) for v in t)
-        if rank != 0:
-            return None
-        assert gathered.shape == (n_streams, pcm_len), gathered.shape
-        sig_s = nb * bb / 2 / rx.geo.rf_fs
-        res = {"workload": f"BASELINE configs[4]: {n_streams} independent mode-{mode} stereo streams x {sig_s:g} s, "
-                           f"{world} rank(s), streams sharded contiguously"
-                           + (", S16 PCM gathered to rank 0" if pg else ", PCM left on the one rank (no gather)"),
-               "n_gpus": world, "seconds": round(total, 4), "seconds_process": round(proc, 4),
-               "seconds_gather": round(gat, 4), "gather_bytes": int(gathered.numel() * 2),
-               "MS_per_s": round(n_streams * nb * bb / 2 / total / 1e6, 1),
-               "stream_seconds_per_s": round(n_streams * sig_s / total, 1),
-               "x_realtime_per_stream": round(sig_s / total, 2), "synth_seconds_untimed": round(t_synth, 3)}
-        if expect:
-            got = {sid: hashlib.sha256(gathered[sid].cpu().numpy().tobytes()).hexdigest() for sid in expect}
-            res["checked_streams"] = sorted(expect)
-            res["bit_exact_vs_reference"] = all(got[sid] == expect[sid] for sid in expect)
-        return res
-    finally:
-        rx.close()
+        return out
+
+    # profile(rx, run) (optional, rank 0): one more call of rank 0's shard, e.g. with the stage
+    # timing armed (bench.stage_latency); its result is the line's `latency`
+    post = None
+    if profile is not None and ids:
+        post = lambda st: profile(st[0], lambda: st[0].process_device(st[1].data_ptr(), nb, st[2].data_ptr()))
+    res = run_leg(setup, process, n_streams, pcm_len, world, rank, pg, dev, cleanup=lambda st: st[0].close(),
+                  post=post)
+    if rank != 0:
+        return None
+    if "error" in res:
+        return {"error": res["error"], "n_gpus": world}
+    gathered = res.pop("gathered")
+    assert gathered.shape == (n_streams, pcm_len), gathered.shape
+    sig_s = nb * bb / 2 / geo.rf_fs
+    total = res["total"]
+    out = {"workload": f"BASELINE configs[4]: {n_streams} independent mode-{mode} stereo streams x {sig_s:g} s, "
+                       f"{world} rank(s), streams sharded contiguously"
+                       + (", S16 PCM gathered to rank 0" if pg else ", PCM left on the one rank (no gather)"),
+           "n_gpus": world, "seconds": round(total, 4), "seconds_process": round(res["process"], 4),
+           "seconds_gather": round(res["gather"], 4), "gather_bytes": int(gathered.numel() * 2),
+           "MS_per_s": round(n_streams * nb * bb / 2 / total / 1e6, 1),
+           "stream_seconds_per_s": round(n_streams * sig_s / total, 1),
+           "x_realtime_per_stream": round(sig_s / total, 2), "synth_seconds_untimed": round(t_synth[0], 3),
+           "dist": {"world_size": dist.get_world_size() if pg else 1,
+                    "backend": ({"nccl": "RCCL"}.get(dist.get_backend(), dist.get_backend()) if pg else None)},
+           "per_rank": [{"rank": r, "streams": len(shard(n_streams, world, r)), "seconds": round(v[0], 4),
+                         "seconds_process": round(v[1], 4), "seconds_gather": round(v[2], 4)}
+                        for r, v in enumerate(res["per_rank"])]}
+    if "post" in res:
+        out["latency"] = res["post"]
+    if expect:
+        got = {sid: hashlib.sha256(gathered[sid].cpu().numpy().tobytes()).hexdigest() for sid in expect}
+        out["checked_streams"] = sorted(expect)
+        out["bit_exact_vs_reference"] = all(got[sid] == expect[sid] for sid in expect)
+    else:
+        out["parity"] = f"unpinned: no reference hashes recorded for {n_streams} streams x {nb} blocks"
+    return out
 
 
 def run_time_sharded(process: Callable[[range], torch.Tensor], n_blocks: int, pcm_per_block: int,

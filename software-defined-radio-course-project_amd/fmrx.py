@@ -87,7 +87,13 @@ PROTOTYPES = {
     "fmrx_test_pll_fallback": (C.c_int, [_vp, C.c_int, _vp, _vp, _sz, _vp]),
     "fmrx_debug_mono_stamps": (C.c_int, [_vp, _vp, _sz, C.POINTER(_sz)]),
     "fmrx_debug_pll_stats": (C.c_int, [_vp, _vp]),
+    "fmrx_debug_stage_timing": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                          C.POINTER(C.c_long), C.c_int]),
 }
+
+# fmrx_debug_stage_timing's stage kinds (csrc/fmrx_internal.h StageKind)
+STAGES = ["front_end", "bandpass_pair", "pll_prep", "runner_lane", "runner_pred", "runner_sat", "runner_pipe20",
+          "runner_pipe21", "runner_pipe22", "pll_check", "pll_tail", "pll_nco", "audio"]
 
 _lib = None
 
@@ -359,6 +365,16 @@ class Receiver:
         need = _sz()
         _check(lib().fmrx_debug_mono_stamps(self.h, d_stamps, n_workgroups, C.byref(need)))
         return need.value
+
+    def stage_timing(self, op: int) -> dict | None:
+        """Per-stage device time of the stereo engine (fmrx_debug_stage_timing): op 1 arms,
+        0 reads, -1 reads and disarms; a read returns {stage: (ms, launches, steps)}."""
+        n = len(STAGES)
+        ms, steps, la = (C.c_double * n)(), (C.c_double * n)(), (C.c_long * n)()
+        _check(lib().fmrx_debug_stage_timing(self.h, op, ms, steps, la, n))
+        if op == 1:
+            return None
+        return {STAGES[k]: (ms[k], la[k], steps[k]) for k in range(n) if la[k]}
 
     def debug_pll_stats(self, d_counts: int | None) -> None:
         """Diagnostic speculative-PLL counters (fmrx.h): d_counts[0] += runner batches that did

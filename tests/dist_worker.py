@@ -47,11 +47,36 @@ def process_time(n_blocks):
     return process
 
 
+def leg_with_failure(d, n_streams, world, rank, where):
+    """dist.run_leg with rank 1 raising in `where` ("setup" or "process"): every rank must
+    return (no rank left in a collective) with the error reported; rank 0 records it."""
+    def setup():
+        if where == "setup" and rank == 1:
+            raise RuntimeError("injected setup failure")
+        return list(d.shard(n_streams, world, rank))
+
+    def run(ids):
+        if where == "process" and rank == 1:
+            raise RuntimeError("injected process failure")
+        return process(ids)
+
+    return d.run_leg(setup, run, n_streams, NB * NA * 2, world, rank, True)
+
+
 def main():
     n_streams, out_path = int(sys.argv[1]), sys.argv[2]
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     d = iqgen.load_module("dist")
+    if len(sys.argv) > 3 and sys.argv[3] in ("setup", "process", "ok"):  # dist.run_leg failure agreement
+        res = leg_with_failure(d, n_streams, world, rank, sys.argv[3])
+        if rank == 0:
+            if "error" in res:
+                np.save(out_path, np.frombuffer(res["error"].encode(), np.uint8))
+            else:
+                np.save(out_path, res["gathered"].numpy())
+        dist.destroy_process_group()
+        return
     if len(sys.argv) > 3 and sys.argv[3] == "time":  # argv[1] = blocks of the one stream
         got = d.run_time_sharded(process_time(n_streams), n_streams, NA, world, rank)
     else:

@@ -40,11 +40,26 @@ def test_bench_json_contract():
     for c in ("configs[2]", "configs[3]"):
         assert oc[c]["input_matches_fixture"] is True, oc[c]
         assert oc[c]["bit_exact_vs_reference"] is True, oc[c]
+        # every config carries its CPU baseline (the reference's own path, oracle/_ref, same bytes)
+        cb = oc[c]["cpu_baseline"]
+        assert cb["kind"] == "reference" and cb["cores"] == 1 and cb["value"] > 0 and cb["bit_exact_vs_gpu"] is True, cb
+    assert oc["configs[2]"]["cpu_baseline"]["threaded_project"]["prefix_bit_exact_vs_gpu"] is True
+    # configs[3] priced against HBM and the no-FMA VALU like the headline; the stereo configs
+    # against the serial chain's instruction floor per PLL regime
+    r3 = oc["configs[3]"]["roofline"]
+    assert 0 < r3["frac"] < 1 and 0 < r3["binding"]["frac"] < 1 and r3["kernel_ms"] > 0
+    for c in ("configs[2]", "configs[4]"):
+        lat = oc[c]["latency"]
+        assert lat["runner_ms"] > 0 and lat["regimes"], lat
+        for k, r in lat["regimes"].items():
+            assert k.startswith("runner_") and 0 < r["frac"] <= 1.0 and r["ns_per_step"] > r["floor_ns_per_step"], (k, r)
     # configs[4] (256 stereo streams; 0.5 s each here, 60 s by default) checked against the
     # reference build's per-stream hashes
     c4 = oc["configs[4]"]
     assert "error" not in c4, c4
     assert c4["n_gpus"] == 1 and c4["checked_streams"] == [0, 7, 8, 15] and c4["bit_exact_vs_reference"] is True
+    # each rank's own split (one rank here) and the process group it ran in
+    assert c4["dist"]["world_size"] == 1 and len(c4["per_rank"]) == 1 and c4["per_rank"][0]["streams"] == 256
     rf = j["roofline"]
     assert rf["bound"] in ("hbm", "mfma") and rf["unit"] in ("GB/s", "TFLOP/s")
     assert 0 < rf["frac"] < 1 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3

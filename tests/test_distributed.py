@@ -64,3 +64,19 @@ def test_time_shards_world2_match_whole_stream(n_blocks, orc, tmp_path):
     whole = iqgen.make("synth:77", n_blocks * BB)
     want = orc.run(MODE, 51, whole, ["pcm_mono"])["pcm_mono"]
     assert got.shape == want.shape and np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("where", ["setup", "process"])
+def test_run_leg_failure_on_one_rank_does_not_hang(where, tmp_path):
+    """A rank that raises before the barrier or before the gather (bench.py's configs[4] step at
+    N > 1) must not leave the other rank blocked in the collective: dist.run_leg agrees on
+    success first, both ranks return, and rank 0 reports the failing rank's error."""
+    got = _run_world2(tmp_path, 3, where)
+    msg = got.tobytes().decode()
+    assert "injected" in msg or "another rank failed" in msg, msg
+
+
+def test_run_leg_world2_gathers(orc, tmp_path):
+    got = _run_world2(tmp_path, 3, "ok")
+    want = np.stack([orc.run(MODE, 51, iqgen.make(f"rand:{100 + i}", NB * BB), ["pcm"])["pcm"] for i in range(3)])
+    assert np.array_equal(got, want)

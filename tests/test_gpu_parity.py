@@ -532,6 +532,27 @@ def test_pll_speculation_fallbacks(fmrx, orc, monkeypatch, env, n_streams, nb):
         assert np.array_equal(out2[0], want2)
 
 
+@pytest.mark.parametrize("skew", [4194304.0, 1048576.0, 16777216.0])
+def test_pll_wrong_hint_fails_safe(fmrx, orc, monkeypatch, skew):
+    """The host picks a segment's runners from its trigOffset bounds (api.cpp TrigTrack).  With
+    the bounds deliberately wrong (test hook FMRX_PLL_HINT_SKEW: the host believes the streams
+    are `skew` samples further on), the runners launched leave the streams alone; the pre-pass's
+    fail[] sentinel (0) then makes pll_kernel resume each such stream's whole segment on the
+    certified path: slower, bit-identical (stats: every checked batch resumed)."""
+    monkeypatch.setenv("FMRX_PLL_HINT_SKEW", str(skew))
+    nb, bb, n_streams = 30, 12800, 3
+    ins = np.stack([iqgen.make(f"synth:{950 + s}", nb * bb) for s in range(n_streams)])
+    with fmrx.Receiver(0, fmrx.STEREO, n_streams=n_streams) as rx:
+        counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+        rx.debug_pll_stats(counts.data_ptr())
+        out = rx.process(ins)
+        rx.debug_pll_stats(None)
+    resumed, checked = counts.cpu().tolist()
+    assert checked > 0 and resumed == checked, (resumed, checked)
+    for s in range(n_streams):
+        assert np.array_equal(out[s], orc.run(0, 51, ins[s], ["pcm"])["pcm"]), s
+
+
 @pytest.mark.parametrize("name", sorted(long_runs()))
 def test_stereo_long_hash(fmrx, name):
     h = long_runs()[name]

@@ -1,0 +1,24 @@
+#!/bin/bash
+# tools/gpu_dev.sh <tag> [steps...] — development GPU call: each named step under its own time
+# limit, stopping at the first failure.  Steps: tests (whole GPU suite), pll (PLL / stereo tests
+# only), stages (tools/stage_times.py), bench (bench.py, no CPU baseline), smoke.
+set -o pipefail
+TAG=${1:-dev}; shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+for step in "$@"; do
+  case $step in
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
+           tail -2 $OUT/tests.log ;;
+    pll) timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "pll or stereo or bench_config or trig_hint or refdata or cli" > $OUT/pll.log 2>&1 || { tail -40 $OUT/pll.log; exit 2; }
+           tail -2 $OUT/pll.log ;;
+    stages) timeout -k 10 300 python tools/stage_times.py > $OUT/stages.json 2> $OUT/stages.err || { tail $OUT/stages.err; exit 3; }
+           cat $OUT/stages.json ;;
+    bench) timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 4; }
+           python -c "import json; j=json.load(open('$OUT/bench.json')); print(j['value'], j['roofline']['kernel_ms'], json.dumps(j.get('baseline_configs',{}))[:1500])" ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail $OUT/smoke.log; exit 5; }
+           tail -1 $OUT/smoke.log ;;
+  esac
+done
+echo all done

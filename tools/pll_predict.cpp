@@ -139,7 +139,7 @@ int main(int argc, char** argv) {
     // candidates), per octave of j -- how many candidates a chain would need there
     std::printf("B-step batches within m floats of c0 (2m + 1 candidates), lookback %d:\n", lb);
     std::printf("%-22s %s\n", "j range", "m = 1 .. 8");
-    for (int B : {16, 32, 64})
+    for (int B : {8, 16, 32, 64})
     for (int e = 17; e < 22; e++) {
         const size_t j0 = (size_t)1 << e, j1 = std::min((size_t)1 << (e + 1), N);
         if (j0 >= j1) continue;
