@@ -218,6 +218,26 @@ class Oracle(_Lib):
         f(out.ctypes.data_as(_dp), C.byref(pv), i.ctypes.data_as(_dp), q.ctypes.data_as(_dp), i.size)
         return out, pv.value
 
+    def mixer(self, a, b):
+        """mixer (filter.cpp:176-184): 2 (a b) in float."""
+        a = np.ascontiguousarray(a, np.float32)
+        b = np.ascontiguousarray(b, np.float32)
+        out = np.zeros(a.size, np.float32)
+        f = self.lib.orc_mixer
+        f.argtypes = [_fp, _fp, _fp, C.c_int]
+        f(_ptr(out, _fp), _ptr(a, _fp), _ptr(b, _fp), a.size)
+        return out
+
+    def lr(self, mono, stereo):
+        """LRExtraction (filter.cpp:186-199): (left, right) = ((m + s) 0.5, (m - s) 0.5)."""
+        m = np.ascontiguousarray(mono, np.float32)
+        st = np.ascontiguousarray(stereo, np.float32)
+        left, right = np.zeros(m.size, np.float32), np.zeros(m.size, np.float32)
+        f = self.lib.orc_lr
+        f.argtypes = [_fp, _fp, _fp, _fp, C.c_int]
+        f(_ptr(left, _fp), _ptr(right, _fp), _ptr(m, _fp), _ptr(st, _fp), m.size)
+        return left, right
+
     def quant(self, x):
         f = self.lib.orc_quant
         f.restype = C.c_int16

@@ -59,7 +59,7 @@ size_t pll_side_doubles(int n, int n_streams);
 // measured, not modelled.
 enum StageKind {
     kStFront, kStBpf, kStPrep, kStLane, kStPred, kStSat, kStPipe20, kStPipe21, kStPipe22, kStCheck, kStTail,
-    kStNco, kStAudio, kStKinds
+    kStNco, kStAudio, kStIdx17, kStIdx18, kStIdx19, kStKinds
 };
 struct StageTimer {
     bool on = false;
@@ -130,6 +130,15 @@ void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_str
 void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
                      float* st, float* out, size_t ostride, int inject, int miss, int form,
                      unsigned long long* stats);
+
+// pll_pred.hip: the index runner (one stream a workgroup of four waves, spw == 1) for trigOffset
+// in [2^17, 2^20), self-certifying like launch_pll_pipe, same arguments; form 17: 64 candidates
+// ([2^17, 2^18)), 18: 32 ([2^18, 2^19)), 19: 16 ([2^19, 2^20)).  A stream outside the form's
+// domain runs the range exactly.
+void launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
+                    float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats);
+constexpr int kPllIdxWaves = 4;  // waves a stream: the chain and three evaluators, one SIMD each
+constexpr float kPllIdxMin = 131072.0f;  // 2^17: the index runner's lowest trigOffset
 
 // test hook: the PLL's fallback libm on device (kind 0 sincos, 1 atan2, 2 NCO cos)
 int launch_pll_fallback_test(int kind, const float* a, const float* b, size_t n, float* out, hipStream_t s);

@@ -1003,6 +1003,261 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     (void)n_inj;
 }
 
+
+// ---- pll_idx_kernel: one stream a workgroup of 1 + NW waves, trigOffset in [2^17, 2^20) ---------
+//
+// Below 2^20 trigArg's float grid (2^-8 .. 2^-5 rad) is finer than the phase moves in the two
+// intervals between a prediction and its use, so three or five candidates miss; 16 to 64 do not
+// (tools/pll_predict.cpp, profiles/r04/pll_predict_below_2_20.txt: 16-step intervals from the
+// phase one interval back hit with 64 candidates on 0.9999+ of them in [2^17, 2^18), with 32 in
+// [2^18, 2^19), with 16 in [2^19, 2^20)).  Compares against NC - 1 thresholds would cost the
+// chain 2 (NC - 1) instructions a step, so here the chain forms the step's trigArg itself --
+// float(P + (double)phase), filter.cpp:165, three instructions -- and turns it into a lane index:
+// the NC candidates of a step c0 - NC/2 .. c0 + NC/2 - 1 sit in NC consecutive lanes of one VGPR
+// row (64 / NC steps a row), so e = v_readlane(row, bits(trigArg) - base) with
+// base = bits(c0) - NC/2 - the step's lane offset:
+//   the chain (wave 0), per step: e from the previous trigArg's lane (v_readlane), (Ki e, Kp e),
+//     the three float updates (filter.cpp:161-162), trigArg (cvt, add_f64, cvt), its lane index
+//     (sub, v_readfirstlane), the index recorded in lane J of a row (v_writelane) -- 11 VALU a
+//     step whatever NC is.  After the interval it tests the row (every index inside its step's
+//     NC lanes) and the phase (not NaN: an uncertified candidate's e is NaN, so a chain that took
+//     one carries NaN from there); a miss is redone on the exact path at once, from the state at
+//     the interval's start (in registers), so it costs 16 exact steps and no pipeline restart: the
+//     evaluators' next interval was predicted from the phase before the missed one, still right;
+//   the evaluators (waves 1 .. NW, one SIMD each), per interval k: interval k + 1's candidate
+//     rows (pred_e_cert for each lane's candidate, NaN where uncertified), P and base of each
+//     step, from the phase at interval k's start; wave 1 also stores interval k - 1's trigArgs
+//     (base + index: the candidate IS the trigArg) unless the chain redid it.
+// So the runner is exact by construction, as pll_pipe_kernel: every e the chain used is a
+// certified candidate's that is the true trigArg.  One launch runs a form's whole range of the
+// call and leaves the exact end state in st.
+template <int NC, int NW>
+__global__ void __launch_bounds__(64 * (1 + NW)) __attribute__((amdgpu_waves_per_eu(1, 1)))
+pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step, float norm_bw, float* st,
+               float* out_base, size_t ostride, int inject, int miss, float lo, float hi, unsigned long long* stats) {
+    constexpr int NI = 16;          // steps an interval
+    constexpr int SPP = 64 / NC;    // steps a candidate row
+    constexpr int NR = NI / SPP;    // candidate rows an interval
+    constexpr int HC = NC / 2;      // candidates c0 - HC .. c0 + HC - 1
+    constexpr int RD = 4;           // intervals of step inputs in flight
+    constexpr int NP = (NR + NW - 1) / NW;  // rows an evaluator wave computes
+    static_assert(NC == 16 || NC == 32 || NC == 64, "a power of two dividing the wave");
+    // rings of four intervals (interval k in slot k & 3): per step (P lo, P hi, base, -) (sp), the
+    // candidate rows (se), the chain's lane index of each step's trigArg (srow), its (integ,
+    // phase) at the interval's end (sst), "redone exactly" (sexact)
+    __shared__ float4 sp[4][NI];
+    __shared__ float se[4][NR][64];
+    __shared__ int srow[4][NI];
+    __shared__ float2 sst[4];
+    __shared__ int sexact[4];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
+    const int s = blockIdx.x;  // grid = n_streams
+    const float* x = io + (size_t)s * stride;
+    float* out = out_base + (size_t)s * ostride;
+    float* S = st + 8 * (size_t)s;
+    const float Kp = norm_bw * static_cast<float>(2.666);
+    const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
+    auto uni = [](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v))); };
+    PllState p{uni(S[0]), uni(S[1]), uni(S[2]), uni(S[3]), uni(S[5])};
+    const bool in_domain = pll_pipe_stream(p.trig, step, lo, hi);
+    const float trig0 = p.trig;
+    const double t0d = (double)trig0;
+    auto pr_at = [&](long long j) {
+        return step * (double)(float)fmin(t0d + (double)(j + 1), (double)kPllTrigStick);
+    };
+    const int nb = n / NI;
+    const int ni = nb > 0 ? nb - 1 : 0;  // intervals after interval 0 (exact)
+    // test hook: a forced miss on interval 1 + (inject + s) % ni (counted as resumed)
+    const int inj = inject >= 0 && ni > 0 ? 1 + (inject + s) % ni : -1;
+    auto exact = [&](PllState& q, PllCtx& c, long long j0, long long j1) {
+        if (j1 > j0) {
+            const PllPair z = pll_redo(q, c, x + j0, out + j0, (int)(j1 - j0), Ki, Kp, step, true);
+            q = z.p;
+            c = z.ctx;
+        }
+    };
+    if (ni < 2 || !in_domain) {
+        if (w == 0) {
+            PllCtx c{};
+            c.valid = false;
+            exact(p, c, 0, n);
+            if (t == 0) {
+                S[0] = p.integ; S[1] = p.phase; S[2] = p.fbI; S[3] = p.fbQ; S[5] = p.trig;
+                if (stats) {
+                    if (!in_domain) atomicAdd(stats, (unsigned long long)nb);
+                    atomicAdd(stats + 1, (unsigned long long)nb);
+                }
+            }
+        }
+        return;
+    }
+    auto j0 = [](int k) { return NI * k; };  // interval k's first step
+
+    if (w > 0) {
+        // this wave's rows r = w - 1 + NW q; lane t: step J = r SPP + t / NC, candidate t % NC
+        float vq[RD][NP];
+        auto ld = [&](int k, float (&v)[NP]) {
+            const int kk = k <= ni ? k : ni;
+#pragma unroll
+            for (int q = 0; q < NP; q++) {
+                const int r = min(w - 1 + NW * q, NR - 1);
+                const int j = j0(kk) + r * SPP + t / NC;
+                v[q] = x[min(j + 1, n - 1)];  // the step the e is for
+            }
+        };
+        auto put = [&](int k, float phase_ref, const float (&v)[NP]) {
+            const int sl = k & 3;
+#pragma unroll
+            for (int q = 0; q < NP; q++) {
+                const int r = w - 1 + NW * q;
+                if (NP * NW > NR && r >= NR) break;
+                const int J = r * SPP + t / NC, kc = t % NC;
+                const int j = j0(k) + J;
+                const double pr = pr_at(j);
+                const uint32_t cb = __builtin_bit_cast(uint32_t, (float)(pr + (double)phase_ref));
+                bool ok;
+                const float e = pred_e_cert(__builtin_bit_cast(float, cb - (uint32_t)HC + (uint32_t)kc), v[q],
+                                            pll_iv(v[q]), ok);
+                // a candidate that is not a positive finite float never certifies: c0 < 2^126
+                const bool fin = cb > (uint32_t)HC && cb < 0x7F000000u;
+                se[sl][r][t] = ok && fin ? e : __builtin_nanf("");
+                if (kc == 0) {
+                    const uint64_t pb = __builtin_bit_cast(uint64_t, pr);
+                    sp[sl][J] = make_float4(__builtin_bit_cast(float, (uint32_t)pb),
+                                            __builtin_bit_cast(float, (uint32_t)(pb >> 32)),
+                                            __builtin_bit_cast(float, cb - (uint32_t)HC - (uint32_t)(NC * (J % SPP))),
+                                            0.0f);
+                }
+            }
+        };
+        // wave 1: interval k's trigArgs, base + the chain's lane index (the chain stored a redone
+        // interval itself)
+        auto store = [&](int k) {
+            if (w != 1) return;
+            const int sl = k & 3;
+            if (sexact[sl]) return;
+            const int J = t & (NI - 1);
+            const float a = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, sp[sl][J].z) + (uint32_t)srow[sl][J]);
+            if (t < NI) out[j0(k) + J] = a;
+        };
+#pragma unroll
+        for (int u = 0; u < RD; u++) ld(1 + u, vq[(1 + u) % RD]);
+        put(1, p.phase, vq[1 % RD]);  // interval 1 from the phase at interval 0's start
+        ld(1 + RD, vq[1 % RD]);
+        __syncthreads();  // (prologue)
+        for (int i0 = 1; i0 <= ni; i0 += RD) {
+            unroll_ic(
+                [&](auto uc) {
+                    constexpr int u = decltype(uc)::value;
+                    constexpr int sl = (2 + u) % RD;  // slot of interval i + 1
+                    const int i = i0 + u;
+                    if (i <= ni) {
+                        if (i + 1 <= ni) {
+                            put(i + 1, sst[(i - 1) & 3].y, vq[sl]);  // from the phase at interval i's start
+                            ld(i + 1 + RD, vq[sl]);
+                        }
+                        store(i - 1);
+                        __syncthreads();
+                    }
+                },
+                std::make_integer_sequence<int, RD>{});
+        }
+        store(ni);
+        return;
+    }
+
+    // ---- the chain
+    PllCtx ctx{};
+    ctx.valid = false;
+    exact(p, ctx, 0, NI);  // interval 0 on the exact path
+    float integ = p.integ, phase = p.phase;
+    // the carry: the candidate row value of the previous trigArg and its lane (SGPR); after an
+    // exact stretch that trigArg's exact e in every lane
+    float cE;
+    uint32_t cL = 0;
+    auto carry_exact = [&](float a, int k) {
+        cE = exact_e(a, x[min(j0(k), n - 1)]);
+        cL = 0;
+    };
+    carry_exact((float)ctx.x, 1);
+    if (t == 0) {
+        sst[0] = make_float2(integ, phase);
+        sexact[0] = 1;
+    }
+    __syncthreads();  // (prologue)
+    unsigned long long n_redo = 0, n_inj = 0;
+    const uint32_t off = (uint32_t)(NC * ((t & (NI - 1)) % SPP));  // lane t's step's lane offset
+    for (int i = 1; i <= ni; i++) {
+        const int is = i & 3;
+        const float integ0 = integ, phase0 = phase;
+        // the interval's data before its steps (NI 16-byte broadcasts, NR row reads)
+        float4 D[NI];
+        float E[NR];
+#pragma unroll
+        for (int J = 0; J < NI; J++) D[J] = sp[is][J];
+#pragma unroll
+        for (int r = 0; r < NR; r++) E[r] = se[is][r][t];
+        __builtin_amdgcn_sched_barrier(0);
+        int row = 0;
+        unroll_ic(
+            [&](auto jc) {
+                constexpr int J = decltype(jc)::value;
+                // step J: e from the previous trigArg's candidate lane, filter.cpp:161-162
+                const float e = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cE), cL));
+                const float2v kv = float2v{Ki, Kp} * e;
+                integ = integ + kv.x;
+                phase = phase + (kv.y + integ);
+                // trigArg (filter.cpp:165) and its lane in step J's candidate row
+                const double P = __builtin_bit_cast(double, make_uint2(__builtin_bit_cast(uint32_t, D[J].x),
+                                                                       __builtin_bit_cast(uint32_t, D[J].y)));
+                const float a = (float)(P + (double)phase);
+                cL = __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, a) - __builtin_bit_cast(uint32_t, D[J].z));
+                cE = E[J / SPP];
+                int rw = row;  // (a local: clang rejects a captured variable as an asm operand here)
+                const uint32_t sl = cL;
+                asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(rw) : "s"(sl), "i"(J));
+                row = rw;
+            },
+            std::make_integer_sequence<int, NI>{});
+        // the interval's verdict: every trigArg's lane inside its step's candidates, no NaN e
+        // taken (the phase), the start state in pll_batch_fast's range; test hooks force misses
+        const bool lane_bad = t < NI && (uint32_t)row - off >= (uint32_t)NC;
+        const bool bad = __builtin_amdgcn_ballot_w64(lane_bad) != 0 || !(phase == phase) ||
+                         !(fabsf(phase0) < kPllMaxPhase && fabsf(integ0) < kPllMaxInteg) || i == min(miss, ni) || i == inj;
+        if (bad) {  // uniform: redo the interval exactly from its start (the chain stores it)
+            n_redo++;
+            n_inj += i == inj ? 1 : 0;
+            const float a = (float)(pr_at(j0(i) - 1) + (double)phase0);  // the trigArg before it
+            PllState q;
+            PllCtx c{};
+            pll_state_at(q, c, integ0, phase0, trig0, (long long)j0(i), a, DeviceLib{});
+            exact(q, c, j0(i), j0(i) + NI);
+            integ = q.integ;
+            phase = q.phase;
+            carry_exact((float)c.x, i + 1);
+        }
+        if (t < NI) srow[is][t] = row;
+        sst[is] = make_float2(integ, phase);
+        sexact[is] = bad ? 1 : 0;
+        __syncthreads();
+    }
+    // the steps past the last interval exactly, from the end state
+    const long long jf = j0(ni + 1);
+    const float a = (float)(pr_at(jf - 1) + (double)phase);
+    PllState q;
+    PllCtx c{};
+    pll_state_at(q, c, integ, phase, trig0, jf, a, DeviceLib{});
+    exact(q, c, jf, n);
+    if (t == 0) {
+        S[0] = q.integ; S[1] = q.phase; S[2] = q.fbI; S[3] = q.fbQ; S[5] = q.trig;
+        if (stats) {
+            atomicAdd(stats, n_inj);  // "resumed": the inject hook's forced redos only
+            atomicAdd(stats + 1, (unsigned long long)nb);
+        }
+    }
+    (void)n_redo;
+}
+
 }  // namespace
 
 #ifdef FMRX_AB_PROF
@@ -1050,6 +1305,21 @@ void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_
     else
         hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 1, 8, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
                            stride, step, norm_bw, st, out, ostride, inject, miss, stats);
+}
+
+void launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
+                    float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats) {
+    if (n <= 0) return;
+    static_assert(kPllIdxWaves == 4, "the chain and three evaluators");
+    if (form == 17)
+        hipLaunchKernelGGL((pll_idx_kernel<64, 3>), dim3(n_streams), dim3(256), 0, s, io, n, n_streams, stride, step,
+                           norm_bw, st, out, ostride, inject, miss, 131072.0f, 262143.0f, stats);
+    else if (form == 18)
+        hipLaunchKernelGGL((pll_idx_kernel<32, 3>), dim3(n_streams), dim3(256), 0, s, io, n, n_streams, stride, step,
+                           norm_bw, st, out, ostride, inject, miss, 262144.0f, 524287.0f, stats);
+    else
+        hipLaunchKernelGGL((pll_idx_kernel<16, 3>), dim3(n_streams), dim3(256), 0, s, io, n, n_streams, stride, step,
+                           norm_bw, st, out, ostride, inject, miss, 524288.0f, 1048575.0f, stats);
 }
 
 }  // namespace fmrx

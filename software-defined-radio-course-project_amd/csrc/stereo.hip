@@ -987,8 +987,15 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     // the three-wave runner: every stream at the same known trigOffset t, a SIMD per wave (one
     // stream a workgroup of three); it takes the samples from trigOffset 2^20 on
     const bool pipe = spec && pred_ok && pipe_env && spw == 1 && 3 * n_streams <= n_simd && k && hlo == hhi;
+    // the index runner below 2^20 wants four SIMDs a stream (FMRX_PLL_IDX=0: not launched)
+    const int idx_env = [] {
+        const char* e = std::getenv("FMRX_PLL_IDX");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    const bool idx = pipe && idx_env && kPllIdxWaves * n_streams <= n_simd;
+    const double fast_min = idx ? (double)kPllIdxMin : (double)kPllPipeMinLow;
     size_t n_seg = (size_t)n;  // samples through the segment loop
-    if (pipe) n_seg = hlo >= (double)kPllPipeMinLow ? 0 : std::min((size_t)n, (size_t)((double)kPllPipeMinLow - hlo));
+    if (pipe) n_seg = hlo >= fast_min ? 0 : std::min((size_t)n, (size_t)(fast_min - hlo));
 
     for (size_t off = 0; off < n_seg; off += seg) {
         // the runners a segment can need (pll_sat_segment / pll_pred_wave take their streams, the
@@ -1062,17 +1069,26 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
                                    spec_stats);
         });
     }
-    // the three-wave runner's ranges: [2^20, 2^21) 16-step five-candidate form, [2^21, 2^22) the
-    // 64-step one, from 2^22 (the stick included) three candidates
+    // the self-certifying runners' ranges: the index runner's [2^17, 2^18) / [2^18, 2^19) /
+    // [2^19, 2^20) forms (64 / 32 / 16 candidates), then the three-wave runner's [2^20, 2^21)
+    // 16-step five-candidate form, [2^21, 2^22) the 64-step one, from 2^22 (the stick included)
+    // three candidates
     for (size_t j = n_seg; pipe && j < (size_t)n;) {
         const double t = std::min(hlo + (double)j, (double)kPllTrigStick);
-        const int form = t < (double)kPllPipeMin5 ? 20 : t < (double)kPllPipeMin ? 21 : 22;
-        const size_t end = form == 20 ? (size_t)((double)kPllPipeMin5 - hlo)
-                         : form == 21 ? (size_t)((double)kPllPipeMin - hlo) : (size_t)n;
-        const size_t e = std::min(end, (size_t)n);
-        timed(form == 20 ? kStPipe20 : form == 21 ? kStPipe21 : kStPipe22, (double)(e - j), [&] {
-            launch_pll_pipe(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j, (size_t)n, inject,
-                            pipe_miss, form, spec_stats);
+        const int form = t < 262144.0 ? 17 : t < 524288.0 ? 18 : t < (double)kPllPipeMinLow ? 19
+                       : t < (double)kPllPipeMin5 ? 20 : t < (double)kPllPipeMin ? 21 : 22;
+        const double edge = form == 17 ? 262144.0 : form == 18 ? 524288.0 : form == 19 ? (double)kPllPipeMinLow
+                          : form == 20 ? (double)kPllPipeMin5 : form == 21 ? (double)kPllPipeMin : 0.0;
+        const size_t e = form == 22 ? (size_t)n : std::min((size_t)(edge - hlo), (size_t)n);
+        const int kind = form == 17 ? kStIdx17 : form == 18 ? kStIdx18 : form == 19 ? kStIdx19
+                       : form == 20 ? kStPipe20 : form == 21 ? kStPipe21 : kStPipe22;
+        timed(kind, (double)(e - j), [&] {
+            if (form < 20)
+                launch_pll_idx(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j, (size_t)n,
+                               inject, pipe_miss, form, spec_stats);
+            else
+                launch_pll_pipe(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j, (size_t)n,
+                                inject, pipe_miss, form, spec_stats);
         });
         j = e;
     }

@@ -93,7 +93,8 @@ PROTOTYPES = {
 
 # fmrx_debug_stage_timing's stage kinds (csrc/fmrx_internal.h StageKind)
 STAGES = ["front_end", "bandpass_pair", "pll_prep", "runner_lane", "runner_pred", "runner_sat", "runner_pipe20",
-          "runner_pipe21", "runner_pipe22", "pll_check", "pll_tail", "pll_nco", "audio"]
+          "runner_pipe21", "runner_pipe22", "pll_check", "pll_tail", "pll_nco", "audio", "runner_idx17", "runner_idx18",
+          "runner_idx19"]
 
 _lib = None
 

@@ -201,3 +201,16 @@ def test_oracle_psd_vs_reference_live(orc, ref):
     assert np.array_equal(f1, f2)
     strong = p2 > p2.max() - PSD_CPP_RANGE_DB
     assert np.abs(p1 - p2)[strong].max() <= PSD_TOL_CPP_DB
+
+
+def test_oracle_mixer_and_lr(orc):
+    """The oracle's mixer (filter.cpp:176-184) and LRExtraction (filter.cpp:186-199), the checkers
+    of the GPU elementwise test: float product then doubling; the float sum/difference times the
+    double 0.5, rounded back to float."""
+    rng = np.random.default_rng(5)
+    a = rng.standard_normal(1000).astype(np.float32)
+    b = rng.standard_normal(1000).astype(np.float32)
+    assert np.array_equal(orc.mixer(a, b), np.float32(2) * (a * b))
+    left, right = orc.lr(a, b)
+    assert np.array_equal(left, ((a + b).astype(np.float64) * 0.5).astype(np.float32))
+    assert np.array_equal(right, ((a - b).astype(np.float64) * 0.5).astype(np.float32))

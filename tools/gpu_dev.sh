@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/gpu_dev.sh <tag> [steps...] — development GPU call: each named step under its own time
 # limit, stopping at the first failure.  Steps: tests (whole GPU suite), pll (PLL / stereo tests
-# only), stages (tools/stage_times.py), bench (bench.py, no CPU baseline), smoke.
+# only), idx (the index-runner tests), ubench (tools/ubench_idx), stages (tools/stage_times.py), bench (bench.py, no CPU baseline), smoke.
 set -o pipefail
 TAG=${1:-dev}; shift
 OUT=gpurun_out/$TAG
@@ -13,6 +13,10 @@ for step in "$@"; do
            tail -2 $OUT/tests.log ;;
     pll) timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "pll or stereo or bench_config or trig_hint or refdata or cli" > $OUT/pll.log 2>&1 || { tail -40 $OUT/pll.log; exit 2; }
            tail -2 $OUT/pll.log ;;
+    idx) timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread -k "index" > $OUT/idx.log 2>&1 || { tail -40 $OUT/idx.log; exit 6; }
+           tail -2 $OUT/idx.log ;;
+    ubench) timeout -k 10 60 tools/ubench_idx > $OUT/ubench_idx.txt 2>&1 || { tail $OUT/ubench_idx.txt; exit 7; }
+           cat $OUT/ubench_idx.txt ;;
     stages) timeout -k 10 300 python tools/stage_times.py > $OUT/stages.json 2> $OUT/stages.err || { tail $OUT/stages.err; exit 3; }
            cat $OUT/stages.json ;;
     bench) timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 4; }

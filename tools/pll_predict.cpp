@@ -137,13 +137,14 @@ int main(int argc, char** argv) {
     }
     // below 2^22: fraction of B-step batches whose every step is within m floats of c0 (2m + 1
     // candidates), per octave of j -- how many candidates a chain would need there
+    const int ms[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 31};
     std::printf("B-step batches within m floats of c0 (2m + 1 candidates), lookback %d:\n", lb);
-    std::printf("%-22s %s\n", "j range", "m = 1 .. 8");
+    std::printf("%-22s %s\n", "j range", "m = 1 2 3 4 6 8 12 16 24 31");
     for (int B : {8, 16, 32, 64})
-    for (int e = 17; e < 22; e++) {
+    for (int e = 14; e < 22; e++) {
         const size_t j0 = (size_t)1 << e, j1 = std::min((size_t)1 << (e + 1), N);
         if (j0 >= j1) continue;
-        long nb_all = 0, ok[9] = {};
+        long nb_all = 0, ok[10] = {};
         for (size_t b0 = j0; b0 + B <= j1; b0 += B) {
             const size_t back = (size_t)(lb - 1) * B + 1;
             const float p0 = phase[b0 - back];
@@ -153,10 +154,10 @@ int main(int argc, char** argv) {
                 kmax = std::max(kmax, std::labs(ulps_between(cand, arg[j])));
             }
             nb_all++;
-            for (int m = 1; m <= 8; m++) ok[m] += kmax <= m;
+            for (int q = 0; q < 10; q++) ok[q] += kmax <= ms[q];
         }
         std::printf("[2^%d, 2^%d)  B=%-3d     ", e, e + 1, B);
-        for (int m = 1; m <= 8; m++) std::printf(" %.4f", (double)ok[m] / nb_all);
+        for (int q = 0; q < 10; q++) std::printf(" %.4f", (double)ok[q] / nb_all);
         std::printf("\n");
     }
     return 0;

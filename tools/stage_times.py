@@ -4,7 +4,9 @@ configs[4] (256 streams x 60 s) and configs[2] (one 1 GiB stream), each call tim
 (wall), then once more with the stage events armed.  ns per PLL step per runner regime from the
 runner launches that ran their segment alone.  One JSON line.
 
-    python tools/stage_times.py [--streams 256] [--seconds 60] [--no-gib]
+    python tools/stage_times.py [--streams 256] [--seconds 60] [--no-gib] [--single 10]
+
+--single S adds one stream of S seconds (the single-stream real-time factor, x_realtime).
 """
 import argparse
 import json
@@ -58,6 +60,7 @@ def main():
     ap.add_argument("--streams", type=int, default=256)
     ap.add_argument("--seconds", type=float, default=60.0)
     ap.add_argument("--no-gib", action="store_true")
+    ap.add_argument("--single", type=float, default=10.0)
     args = ap.parse_args()
     import torch
 
@@ -68,6 +71,11 @@ def main():
     out = {}
     nb = int(args.seconds * 2.4e6 * 2 // 12800)
     out["configs[4]"] = run(fm, args.streams, nb, list(range(args.streams)))
+    if args.single > 0:
+        nb1 = int(args.single * 2.4e6 * 2 // 12800)
+        r = run(fm, 1, nb1, [3000], reps=3)
+        r["x_realtime"] = round(nb1 * 12800 / 2 / 2.4e6 / min(r["wall_s"]), 1)
+        out["single_%gs" % args.single] = r
     if not args.no_gib:
         out["configs[2]"] = run(fm, 1, (1 << 30) // 12800, [3000])
     print(json.dumps(out), flush=True)
