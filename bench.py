@@ -316,10 +316,11 @@ def main() -> None:
 
 # Serial-chain floors of the PLL runners (the stereo configs are latency-bound):
 # VALU instructions a step on the runner's critical wave (csrc/pll_pred.hip chain4_3 /
-# chain4_5, stereo.hip pll_spec_lane_kernel, pll_sat.hip) x ~4.2 cycles a wave64 VALU issue on
+# chain4_5, pll_idx_kernel, stereo.hip pll_spec_lane_kernel, pll_sat.hip) x ~4.2 cycles a wave64 VALU issue on
 # gfx950 (tools/ubench_dep.hip, profiles/r03/ubench_dep.txt), at the 2.4 GHz peak engine clock
 CHAIN_VALU_PER_STEP = {"runner_lane": 35.5, "runner_pred": 16.0, "runner_sat": 8.0, "runner_pipe20": 12.0,
-                       "runner_pipe21": 12.0, "runner_pipe22": 9.0}
+                       "runner_pipe21": 12.0, "runner_pipe22": 9.0, "runner_idx17": 11.0, "runner_idx18": 11.0,
+                       "runner_idx19": 11.0}
 VALU_ISSUE_CYCLES = 4.2
 PEAK_CLOCK_GHZ = 2.4
 

@@ -939,7 +939,9 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         sexact[is] = 0;
         if (__builtin_amdgcn_readfirstlane(flag)) {
             n_redo++;
-            n_inj += flag == 2 ? 1 : 0;
+            // the inject hook's interval counts once it is redone, whichever verdict started the
+            // redo (a real miss on the interval before it clears the hook's own verdict)
+            n_inj += (inj >= i - 2 && inj <= i) ? 1 : 0;
             __syncthreads();  // E2's stores of interval i - 1 happen before the redo's
             // intervals i - 2 (missed), i - 1 and i exactly, from the state at the start of i - 2
             // (the end of interval i - 3 in the ring; interval 0 is batch 0, slot 0 holds its end)
@@ -983,8 +985,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         // fmrx_debug_pll_stats: batches run; "resumed" only for the inject hook's forced redos
         // (the runner is exact by construction: its own redos of missed intervals are internal)
         if (stats) {
-            int fin = 0;  // the verdicts read after the loop
-            for (int k = ni - 1; k <= ni; k++) fin += smiss[k & 3] == 2 ? 1 : 0;
+            const int fin = inj >= f ? 1 : 0;  // the hook's interval redone after the loop
             atomicAdd(stats, (n_inj + (unsigned long long)fin) * 3 * BPI);
             atomicAdd(stats + 1, (unsigned long long)nb);
         }
