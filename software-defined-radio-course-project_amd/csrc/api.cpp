@@ -121,6 +121,10 @@ struct fmrx_ctx {
     unsigned long long* stamps = nullptr;  // fmrx_debug_mono_stamps (diagnostic)
     unsigned long long* pll_stats = nullptr;  // fmrx_debug_pll_stats (diagnostic)
     StageTimer stage_timer;                   // fmrx_debug_stage_timing (diagnostic)
+    // the pipelined stereo engine (run_stereo_pipelined): front-end / band-pass stream, audio
+    // stream and their events, created at the first pipelined call
+    hipStream_t s_front = nullptr, s_audio = nullptr;
+    std::vector<hipEvent_t> pipe_ev;
     int n_simd = 1024;                        // SIMDs of cfg.device (4 per CU), set at creation
     // bounds on the streams' trigOffset (PllHint) of the stereo and the RDS PLL: 0 after a reset,
     // advanced by every call's samples (the float increments stick at 2^24), re-read from the
@@ -291,15 +295,24 @@ int mono_older_share(const fmrx_ctx* c, int segs) {
 }
 
 // RF front end (+ the mono audio stage when `pcm` is non-null and the mode allows it).
+// Chunk form (the stereo pipeline, run_stereo_pipelined): blocks [b0, b0 + n_blocks) of a call of
+// call_blocks blocks a stream starting at d_iq, on stream `st`; the halo of a chunk past the first
+// is the call's own bytes in front of it, and only the last chunk (`last`) moves the context's halo.
 int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm, float* d_mono,
-              float* d_demod, size_t demod_stride, int demod_hist, bool with_audio) {
+              float* d_demod, size_t demod_stride, int demod_hist, bool with_audio, size_t b0 = 0,
+              size_t call_blocks = 0, hipStream_t st = nullptr, bool last = true) {
     const int ns = c->cfg.n_streams;
+    const size_t bb = c->geo.block_bytes;
+    if (call_blocks == 0) call_blocks = n_blocks;
+    if (!st) st = c->stream;
     MonoLaunch L{};
-    L.iq = d_iq;
-    L.halo = c->d_halo[c->halo_cur].p;
+    L.iq = d_iq + b0 * bb;
+    L.iq_stride = call_blocks * bb;
+    L.halo = b0 == 0 ? c->d_halo[c->halo_cur].p : d_iq + b0 * bb - c->halo_bytes;
+    L.halo_stride = b0 == 0 ? c->halo_bytes : L.iq_stride;
     L.pcm = d_pcm;
     L.mono = d_mono;
-    L.demod = d_demod;
+    L.demod = d_demod ? d_demod + b0 * c->geo.if_samples : nullptr;
     L.demod_stride = demod_stride;
     L.demod_hist = demod_hist;
     // When this call produces the mono audio itself, the mono product's audio history stays in
@@ -320,9 +333,10 @@ int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
     // the halo update rides in the fused kernel when every stream row is 16-B aligned (halo
     // bytes and block bytes are multiples of 16); otherwise halo_kernel runs after it
     const char* he = std::getenv("FMRX_HALO_KERNEL");  // =1: the separate halo_kernel (A/B timing)
-    const bool fused_halo = (reinterpret_cast<uintptr_t>(d_iq) & 15) == 0 && L.stream_bytes % 16 == 0 &&
-                            c->halo_bytes % 16 == 0 && !(he && he[0] == '1');
-    L.halo_next = fused_halo ? c->d_halo[c->halo_cur ^ 1].p : nullptr;
+    const bool fused_halo = (reinterpret_cast<uintptr_t>(L.iq) & 15) == 0 && L.stream_bytes % 16 == 0 &&
+                            L.iq_stride % 16 == 0 && c->halo_bytes % 16 == 0 &&
+                            !(he && he[0] == '1');
+    L.halo_next = (last && fused_halo) ? c->d_halo[c->halo_cur ^ 1].p : nullptr;
     const int ad = c->geo.audio_up == 1 ? c->geo.audio_down : 5;
     std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
     if (c->timing) {
@@ -333,18 +347,19 @@ int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
             c->evs.push_back(e);
         }
         ev = &c->evs[c->ev_used++];
-        HIPCHK(hipEventRecord(ev->first, c->stream));
+        HIPCHK(hipEventRecord(ev->first, st));
     }
-    const int st_t = (!with_audio && d_demod) ? c->stage_timer.begin(c->stream) : -1;
+    const int st_t = (!with_audio && d_demod) ? c->stage_timer.begin(st) : -1;
     int rc = launch_mono_fused(L, ns, c->geo.rf_taps, c->geo.rf_decim, c->geo.audio_up,
-                               c->geo.audio_up == 1 ? ad : c->geo.audio_down, c->mono_taps, c->stream);
-    c->stage_timer.end(st_t, kStFront, 0.0, c->stream);
+                               c->geo.audio_up == 1 ? ad : c->geo.audio_down, c->mono_taps, st);
+    c->stage_timer.end(st_t, kStFront, 0.0, st);
     if (rc != 0) return fail(rc == -1 ? FMRX_EINVAL : FMRX_EHIP, "fused kernel launch failed (%d)", rc);
-    if (ev) HIPCHK(hipEventRecord(ev->second, c->stream));
+    if (ev) HIPCHK(hipEventRecord(ev->second, st));
     if (with_audio) c->audio_hist_stale = false;  // demod_tail rewrote the audio history
-    if (!fused_halo) {
-        rc = launch_halo_update(d_iq, L.stream_bytes, c->d_halo[c->halo_cur].p, c->d_halo[c->halo_cur ^ 1].p,
-                                c->halo_bytes, ns, c->stream);
+    if (!last) return 0;
+    if (!L.halo_next) {  // the whole call's tail (every chunk's bytes are in d_iq)
+        rc = launch_halo_update(d_iq, call_blocks * bb, c->d_halo[c->halo_cur].p, c->d_halo[c->halo_cur ^ 1].p,
+                                c->halo_bytes, ns, st);
         if (rc != 0) return fail(FMRX_EHIP, "halo update failed");
     }
     c->halo_cur ^= 1;
@@ -394,6 +409,7 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
     S.channel = c->d_channel.p;
     S.carrier = c->d_carrier.p;
     S.n_if = (int)n_if;
+    S.out_stride = n_if;
     S.hist = kDemodHist;
     S.demod_stride = c->demod_stride;
     S.ch_c = c->ch.data();
@@ -435,6 +451,117 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
     if (launch_copy_streams(c->d_demod.p, c->demod_stride, c->d_demod.p + n_if, c->demod_stride, kDemodHist, ns,
                             c->stream))
         return fail(FMRX_EHIP, "demod history copy failed");
+    return 0;
+}
+
+// Chunks of the stereo pipeline for a call of n_blocks blocks a stream: the stage work beside
+// the serial PLL (front end, band-pass pair, audio) grows with the streams, the PLL's with the
+// samples a stream, so a call pipelines when it has many streams and enough blocks a chunk.
+// FMRX_STEREO_CHUNKS=k forces k chunks (1: the serial engine).
+int stereo_chunks(const fmrx_ctx* c, size_t n_blocks) {
+    if (const char* e = std::getenv("FMRX_STEREO_CHUNKS"))  // at least a block a chunk
+        return (int)std::min<size_t>((size_t)std::max(1, std::atoi(e)), std::max<size_t>(n_blocks, 1));
+    int k = c->cfg.n_streams >= 64 ? 8 : 1;
+    while (k > 1 && n_blocks * c->geo.if_samples / (size_t)k < 16384) k--;  // >= 2^14 samples a chunk
+    return k;
+}
+
+// The stereo engine over the call's blocks in K chunks, pipelined like project.cpp's two threads
+// and their queue (rf_thread / audio_thread, project.cpp:17,71-80,133-141): the context stream
+// runs the serial PLL of chunk k (launch_pll over its samples, the state carried in d_pll),
+// s_front the front end and band-pass pair of chunk k + 1 ahead of it, s_audio the audio stage of
+// chunk k - 1 behind it.  Every chunk reads the call's buffers (demod with its history, channel,
+// carrier/NCO) at its offset, so each stage sees exactly the serial engine's inputs: the same
+// bits.  Events order chunk k's PLL after its band-pass and its audio after its PLL; the call
+// ends with the context stream waiting for the audio stream.
+int run_stereo_pipelined(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm, float* d_mono, int K) {
+    const int ns = c->cfg.n_streams;
+    const size_t ipb = c->geo.if_samples, n_if = n_blocks * ipb;
+    if (c->halo_bytes > c->geo.block_bytes) return fail(FMRX_EINVAL, "halo larger than a block");
+    int rc = c->d_channel.ensure(n_if * ns);
+    if (!rc) rc = c->d_carrier.ensure(n_if * ns);
+    if (rc) return rc;
+    if (!c->s_front) {
+        HIPCHK(hipStreamCreateWithFlags(&c->s_front, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&c->s_audio, hipStreamNonBlocking));
+    }
+    const size_t n_ev = 2 * (size_t)K + 2;
+    while (c->pipe_ev.size() < n_ev) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->pipe_ev.push_back(e);
+    }
+    hipEvent_t ev_start = c->pipe_ev[0], ev_end = c->pipe_ev[1];
+    auto ev_bp = [&](int k) { return c->pipe_ev[2 + 2 * (size_t)k]; };
+    auto ev_pll = [&](int k) { return c->pipe_ev[3 + 2 * (size_t)k]; };
+    // both side streams start after everything enqueued on the context stream so far
+    HIPCHK(hipEventRecord(ev_start, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->s_front, ev_start, 0));
+    HIPCHK(hipStreamWaitEvent(c->s_audio, ev_start, 0));
+    if ((rc = c->d_pll_side.ensure(pll_side_doubles((int)((n_blocks + K - 1) / K * ipb), ns)))) return rc;
+    AudioLaunch A{};
+    A.demod = c->d_demod.p;
+    A.demod_stride = c->demod_stride;
+    A.hist = kDemodHist;
+    A.channel = c->d_channel.p;
+    A.nco = c->d_carrier.p;
+    A.mix_tail = c->d_mix_tail.p;
+    A.mono_state = c->d_mono_state.p;
+    A.pcm = d_pcm;
+    A.mono_out = d_mono;
+    A.n_blocks = (int)n_blocks;
+    A.if_per_block = (int)ipb;
+    A.frames_per_block = (int)c->geo.audio_frames;
+    A.up = c->geo.audio_up;
+    A.down = c->geo.audio_down;
+    A.at = c->geo.audio_taps_total;
+    A.audio_c = c->d_audio.p;
+    for (int k = 0; k < K; k++) {
+        const size_t b0 = n_blocks * (size_t)k / K, b1 = n_blocks * (size_t)(k + 1) / K;
+        const size_t nb = b1 - b0, m = nb * ipb, off = b0 * ipb;
+        const bool last = k == K - 1;
+        // s_front: front end and band-pass pair of chunk k
+        if ((rc = run_fused(c, d_iq, nb, nullptr, nullptr, c->d_demod.p, c->demod_stride, kDemodHist, false, b0,
+                            n_blocks, c->s_front, last)))
+            return rc;
+        StereoLaunch S{};
+        S.demod = c->d_demod.p + off;
+        S.channel = c->d_channel.p + off;
+        S.carrier = c->d_carrier.p + off;
+        S.n_if = (int)m;
+        S.out_stride = n_if;
+        S.hist = kDemodHist;
+        S.demod_stride = c->demod_stride;
+        S.ch_c = c->ch.data();
+        S.ca_c = c->ca.data();
+        S.bp_taps = c->geo.bp_taps;
+        const int t_bp = c->stage_timer.begin(c->s_front);
+        if (launch_bpf_pair(S, ns, c->s_front)) return fail(FMRX_EHIP, "band-pass launch failed");
+        c->stage_timer.end(t_bp, kStBpf, 0.0, c->s_front);
+        HIPCHK(hipEventRecord(ev_bp(k), c->s_front));
+        // the context stream: the PLL of chunk k (project.cpp:166)
+        HIPCHK(hipStreamWaitEvent(c->stream, ev_bp(k), 0));
+        if (launch_pll(c->d_carrier.p + off, (int)m, ns, n_if, 19000.0f, (float)c->geo.if_fs, 2.0f, 0.0f, 0.01f,
+                       c->d_pll.p, c->d_pll_side.p, c->stream, c->hint(c->pll_trig), c->pll_stats)) {
+            c->pll_trig.known = false;
+            return fail(FMRX_EHIP, "PLL launch failed");
+        }
+        c->pll_trig.advance(m);
+        HIPCHK(hipEventRecord(ev_pll(k), c->stream));
+        // s_audio: the audio stage of chunk k (and the state carry after the last)
+        HIPCHK(hipStreamWaitEvent(c->s_audio, ev_pll(k), 0));
+        const int t_au = c->stage_timer.begin(c->s_audio);
+        if (launch_stereo_audio_range(A, (int)b0, (int)b1, last, ns, c->s_audio))
+            return fail(FMRX_EHIP, "stereo audio launch failed");
+        c->stage_timer.end(t_au, kStAudio, 0.0, c->s_audio);
+    }
+    // demod history for the next call (after every read of this call's demod: the last audio
+    // launch follows every band-pass launch through the events)
+    if (launch_copy_streams(c->d_demod.p, c->demod_stride, c->d_demod.p + n_if, c->demod_stride, kDemodHist, ns,
+                            c->s_audio))
+        return fail(FMRX_EHIP, "demod history copy failed");
+    HIPCHK(hipEventRecord(ev_end, c->s_audio));
+    HIPCHK(hipStreamWaitEvent(c->stream, ev_end, 0));
     return 0;
 }
 
@@ -618,6 +745,11 @@ void fmrx_destroy(fmrx_ctx* c) {
         (void)hipEventDestroy(e.second);
     }
     c->stage_timer.release();
+    if (c->s_front) (void)hipStreamSynchronize(c->s_front);
+    if (c->s_audio) (void)hipStreamSynchronize(c->s_audio);
+    for (auto e : c->pipe_ev) (void)hipEventDestroy(e);
+    if (c->s_front) (void)hipStreamDestroy(c->s_front);
+    if (c->s_audio) (void)hipStreamDestroy(c->s_audio);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -774,6 +906,8 @@ int fmrx_process_device_ex(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, in
     if (c->cfg.channels == FMRX_MONO)  // every mode: RF + demod + audio resampler in one launch
         return run_fused(c, d_iq, n_blocks, d_pcm, d_mono, nullptr, 0, 0, true);
     if ((rc = ensure_demod(c, n_if))) return rc;
+    const int K = stereo_chunks(c, n_blocks);
+    if (K > 1) return run_stereo_pipelined(c, d_iq, n_blocks, d_pcm, d_mono, K);
     if ((rc = run_fused(c, d_iq, n_blocks, nullptr, nullptr, c->d_demod.p, c->demod_stride,
                         kDemodHist, false)))
         return rc;

@@ -31,9 +31,11 @@ int launch_halo_update(const uint8_t* iq, size_t stream_bytes, const uint8_t* ol
 // ---- stereo engine (REF_EXACT) kernels -----------------------------------------------
 struct StereoLaunch {
     const float* demod;     // n_streams x (hist + n_if): hist demod samples precede each call
-    float* channel;         // n_streams x n_if
-    float* carrier;         // n_streams x n_if (PLL in place -> NCO)
-    int n_if;               // IF samples this call per stream
+    float* channel;         // n_streams x out_stride
+    float* carrier;         // n_streams x out_stride (PLL in place -> NCO)
+    int n_if;               // IF samples this launch per stream
+    size_t out_stride;      // floats between streams in channel / carrier (n_if, or the whole
+                            //   call's when this launch is a chunk of a longer call)
     int hist;               // demod history length kept in front (>= taps-1)
     size_t demod_stride;    // floats between streams in demod
     const float* ch_c;      // bp taps, HOST memory (passed to the kernel by value)
@@ -138,7 +140,11 @@ void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_
 void launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
                     float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats);
 constexpr int kPllIdxWaves = 4;  // waves a stream: the chain and three evaluators, one SIMD each
-constexpr float kPllIdxMin = 131072.0f;  // 2^17: the index runner's lowest trigOffset
+// the index runner's lowest trigOffset: 2^18.  Its 64-candidate form for [2^17, 2^18) is slower
+// than the lane runner there (113 vs 75 ns a step: 1,024 candidate evaluations an interval on its
+// three evaluator waves, profiles/r04/val/stages.json), so it runs only with FMRX_PLL_IDX=2
+constexpr float kPllIdxMin = 262144.0f;
+constexpr float kPllIdxMin64 = 131072.0f;
 
 // test hook: the PLL's fallback libm on device (kind 0 sincos, 1 atan2, 2 NCO cos)
 int launch_pll_fallback_test(int kind, const float* a, const float* b, size_t n, float* out, hipStream_t s);
@@ -157,6 +163,10 @@ struct AudioLaunch {
     int up, down, at;       // audio resampler
     const float* audio_c;
 };
+// The audio stage of blocks [b0, b1) of the call (the blocks before b0 already computed: their
+// demod / channel / NCO feed b0's histories), then, when `last`, the state carry of the call's
+// last block.  launch_stereo_audio: all of them.
+int launch_stereo_audio_range(const AudioLaunch& L, int b0, int b1, bool last, int n_streams, hipStream_t s);
 int launch_stereo_audio(const AudioLaunch& L, int n_streams, hipStream_t s);
 
 // ---- RDS front half (project.cpp:200-271) ----------------------------------------------

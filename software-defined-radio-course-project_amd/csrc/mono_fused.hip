@@ -205,8 +205,8 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
         const size_t words = L.halo_bytes / 16, total = words * (size_t)(gridDim.x / L.segs);
         for (size_t i = (size_t)blockIdx.x * NT + tid; i < total; i += (size_t)gridDim.x * NT) {
             const size_t s = i / words, j = i - s * words, v = L.stream_bytes + 16 * j;  // into halo ++ iq
-            const uint4 w = v < L.halo_bytes ? *reinterpret_cast<const uint4*>(L.halo + s * L.halo_bytes + v)
-                                             : *reinterpret_cast<const uint4*>(L.iq + s * L.stream_bytes + (v - L.halo_bytes));
+            const uint4 w = v < L.halo_bytes ? *reinterpret_cast<const uint4*>(L.halo + s * L.halo_stride + v)
+                                             : *reinterpret_cast<const uint4*>(L.iq + s * L.iq_stride + (v - L.halo_bytes));
             *reinterpret_cast<uint4*>(L.halo_next + s * L.halo_bytes + 16 * j) = w;
         }
     }
@@ -224,8 +224,8 @@ __global__ void __launch_bounds__(NT) mono_fused_kernel(MonoLaunch L, MonoTaps t
     }
     const long long n_audio = n_if * AU / AD;
 
-    const uint8_t* in = L.iq + (size_t)stream * L.stream_bytes;
-    const uint8_t* halo = L.halo + (size_t)stream * L.halo_bytes;
+    const uint8_t* in = L.iq + (size_t)stream * L.iq_stride;
+    const uint8_t* halo = L.halo + (size_t)stream * L.halo_stride;
     const long long total = (long long)L.stream_bytes;
     const long long hb = (long long)L.halo_bytes;
 

@@ -47,6 +47,10 @@ struct MonoLaunch {
     uint8_t* halo_next;         // optional: the halo after this call (last halo_bytes of halo ++
                                 //   iq per stream), written by the kernel in 16-B words; the
                                 //   caller guarantees 16-B aligned iq rows (else null + halo_kernel)
+    size_t iq_stride;           // bytes between streams in iq (stream_bytes, or the whole call's
+                                //   when this launch is a chunk of a longer call)
+    size_t halo_stride;         // bytes between streams in halo (halo_bytes, or iq_stride when the
+                                //   halo is the call's own bytes in front of the chunk)
 };
 
 // Halo bytes the fused kernel needs in front of a call (pre-roll chunk + RF history).

@@ -12,6 +12,14 @@
 namespace fmrx {
 namespace {
 
+// A/B experiment (Makefile `ab`, AB=-DFMRX_AB_PRIO): the serial PLL runners' waves at the highest
+// issue priority, so parallel kernels sharing their SIMDs take only the issue slots they leave
+#ifdef FMRX_AB_PRIO
+#define FMRX_RUNNER_PRIO() __builtin_amdgcn_s_setprio(3)
+#else
+#define FMRX_RUNNER_PRIO() ((void)0)
+#endif
+
 // src/filter.cpp:136-174 PLL.  A nonlinear recurrence: strictly serial in time, so one lane
 // per stream.  Float state; the reference's double atan2 / cos / sin results rounded to
 // float come from pll_math.h's certified fast path (fallback: the full library call).

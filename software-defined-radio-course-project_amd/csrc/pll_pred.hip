@@ -48,6 +48,7 @@ namespace fmrx {
 // barrier wait, summed over every batch and workgroup, printed at exit
 __device__ unsigned long long g_pred_prof[6];
 __device__ unsigned long long g_pipe_prof[6];
+__device__ unsigned long long g_idx_prof[6];
 #define PROF_T() __builtin_amdgcn_s_memtime()
 #else
 #define PROF_T() 0ull
@@ -214,6 +215,7 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
                                                       const float* st, float* out_base, size_t ostride, int* fail,
                                                       float2* rec, size_t rb, int inject, int sat_ok,
                                                       int pipe_on) {
+    FMRX_RUNNER_PRIO();
     // per step of the batch, double-buffered by batch parity: the phase thresholds of c0 and
     // c0 + 1 ulp, the bits of c0 - 1 ulp and the next step's e for c0 - 1 ulp (sa); its e for c0
     // and c0 + 1 ulp and P (sb: e_0, e_p, P as two words).  Two 16-B reads a step: the chain
@@ -570,6 +572,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                                                       double step, float norm_bw, float* st, float* out_base,
                                                       size_t ostride, int inject, int miss,
                                                       unsigned long long* stats) {
+    FMRX_RUNNER_PRIO();
     constexpr int NI = NB * BPI;
     static_assert(NI == 16 || NI == 32 || NI == 64, "the evaluators' lane map: 64 / NI lanes a step");
     static_assert(NC == 3 || NC == 5, "three or five candidates");
@@ -1036,6 +1039,7 @@ template <int NC, int NW>
 __global__ void __launch_bounds__(64 * (1 + NW)) __attribute__((amdgpu_waves_per_eu(1, 1)))
 pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step, float norm_bw, float* st,
                float* out_base, size_t ostride, int inject, int miss, float lo, float hi, unsigned long long* stats) {
+    FMRX_RUNNER_PRIO();
     constexpr int NI = 16;          // steps an interval
     constexpr int SPP = 64 / NC;    // steps a candidate row
     constexpr int NR = NI / SPP;    // candidate rows an interval
@@ -1146,6 +1150,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         put(1, p.phase, vq[1 % RD]);  // interval 1 from the phase at interval 0's start
         ld(1 + RD, vq[1 % RD]);
         __syncthreads();  // (prologue)
+        unsigned long long ev_body = 0, ev_wait = 0;
         for (int i0 = 1; i0 <= ni; i0 += RD) {
             unroll_ic(
                 [&](auto uc) {
@@ -1153,17 +1158,29 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
                     constexpr int sl = (2 + u) % RD;  // slot of interval i + 1
                     const int i = i0 + u;
                     if (i <= ni) {
+                        const unsigned long long p0 = PROF_T();
                         if (i + 1 <= ni) {
                             put(i + 1, sst[(i - 1) & 3].y, vq[sl]);  // from the phase at interval i's start
                             ld(i + 1 + RD, vq[sl]);
                         }
                         store(i - 1);
+                        const unsigned long long p1 = PROF_T();
                         __syncthreads();
+                        ev_body += p1 - p0;
+                        ev_wait += PROF_T() - p1;
                     }
                 },
                 std::make_integer_sequence<int, RD>{});
         }
         store(ni);
+#ifdef FMRX_AB_PROF
+        if (t == 0 && w == 1) {
+            atomicAdd(&g_idx_prof[2], ev_body);
+            atomicAdd(&g_idx_prof[3], ev_wait);
+        }
+#endif
+        (void)ev_body;
+        (void)ev_wait;
         return;
     }
 
@@ -1186,9 +1203,10 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         sexact[0] = 1;
     }
     __syncthreads();  // (prologue)
-    unsigned long long n_redo = 0, n_inj = 0;
+    unsigned long long n_redo = 0, n_inj = 0, ch_body = 0, ch_wait = 0;
     const uint32_t off = (uint32_t)(NC * ((t & (NI - 1)) % SPP));  // lane t's step's lane offset
     for (int i = 1; i <= ni; i++) {
+        const unsigned long long p0 = PROF_T();
         const int is = i & 3;
         const float integ0 = integ, phase0 = phase;
         // the interval's data before its steps (NI 16-byte broadcasts, NR row reads)
@@ -1240,8 +1258,21 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         if (t < NI) srow[is][t] = row;
         sst[is] = make_float2(integ, phase);
         sexact[is] = bad ? 1 : 0;
+        const unsigned long long p1 = PROF_T();
         __syncthreads();
+        ch_body += p1 - p0;
+        ch_wait += PROF_T() - p1;
     }
+#ifdef FMRX_AB_PROF
+    if (t == 0) {
+        atomicAdd(&g_idx_prof[0], ch_body);
+        atomicAdd(&g_idx_prof[1], ch_wait);
+        atomicAdd(&g_idx_prof[4], (unsigned long long)ni);
+        atomicAdd(&g_idx_prof[5], n_redo);
+    }
+#endif
+    (void)ch_body;
+    (void)ch_wait;
     // the steps past the last interval exactly, from the end state
     const long long jf = j0(ni + 1);
     const float a = (float)(pr_at(jf - 1) + (double)phase);
@@ -1273,6 +1304,10 @@ static void print_pred_prof() {
         std::fprintf(stderr, "pll_pred prof: batches %llu chain body %.1f wait %.1f, evaluator body %.1f wait %.1f "
                      "(shader cycles per batch)\n", h[4], (double)h[0] / h[4], (double)h[1] / h[4],
                      (double)h[2] / h[4], (double)h[3] / h[4]);
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_idx_prof), sizeof h) == hipSuccess && h[4])
+        std::fprintf(stderr, "pll_idx prof: intervals %llu chain body %.1f wait %.1f, evaluator body %.1f wait %.1f "
+                     "(shader cycles per interval), %llu redos\n", h[4], (double)h[0] / h[4], (double)h[1] / h[4],
+                     (double)h[2] / h[4], (double)h[3] / h[4], h[5]);
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pipe_prof), sizeof h) == hipSuccess && h[4])
         std::fprintf(stderr, "pll_pipe prof: intervals %llu chain body %.1f wait %.1f, evaluator body %.1f wait %.1f "
                      "(shader cycles per interval), %llu redos\n", h[4], (double)h[0] / h[4], (double)h[1] / h[4],
@@ -1310,6 +1345,9 @@ void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_
 
 void launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
                     float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats) {
+#ifdef FMRX_AB_PROF
+    reg_pred_prof();
+#endif
     if (n <= 0) return;
     static_assert(kPllIdxWaves == 4, "the chain and three evaluators");
     if (form == 17)

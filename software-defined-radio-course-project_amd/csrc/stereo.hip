@@ -47,8 +47,8 @@ __global__ void __launch_bounds__(256) bpf_pair_kernel(StereoLaunch L, BpTaps t)
         const float2v p = float2v{t.c[k].x, t.c[k].y} * xv;
         acc = acc + p;
     }
-    L.channel[(size_t)s * L.n_if + j] = acc.x;
-    L.carrier[(size_t)s * L.n_if + j] = acc.y;
+    L.channel[(size_t)s * L.out_stride + j] = acc.x;
+    L.carrier[(size_t)s * L.out_stride + j] = acc.y;
 }
 
 // The same FIR pair tiled through LDS: a workgroup stages kBpTile outputs' demod samples plus
@@ -103,8 +103,8 @@ __global__ void __launch_bounds__(kBpThreads) bpf_pair_tile_kernel(StereoLaunch 
 #pragma unroll
     for (int r = 0; r < kBpR; r++) {
         if (j + r < L.n_if) {
-            L.channel[(size_t)s * L.n_if + j + r] = acc[r].x;
-            L.carrier[(size_t)s * L.n_if + j + r] = acc[r].y;
+            L.channel[(size_t)s * L.out_stride + j + r] = acc[r].x;
+            L.carrier[(size_t)s * L.out_stride + j + r] = acc[r].y;
         }
     }
 }
@@ -121,8 +121,8 @@ __global__ void bpf_pair_generic(StereoLaunch L, BpTaps t) {
         a = a + pa;
         b = b + pb;
     }
-    L.channel[(size_t)s * L.n_if + j] = a;
-    L.carrier[(size_t)s * L.n_if + j] = b;
+    L.channel[(size_t)s * L.out_stride + j] = a;
+    L.carrier[(size_t)s * L.out_stride + j] = b;
 }
 
 // Side data of one PLL segment (pll_math.h pll_side): iv, pr for every sample, in
@@ -229,6 +229,7 @@ __global__ void __launch_bounds__(256) pll_kernel(float* io, int n, int n_stream
                                                  const double* side, size_t seg, double step, float norm_bw,
                                                  float* st, float* out_base, size_t ostride, const int* fail,
                                                  const float2* rec, size_t rb, unsigned long long* stats) {
+    FMRX_RUNNER_PRIO();
     const int t = threadIdx.x & 63;
     const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int s_lane = wave * spw + (SPLIT ? ((t >> 4) & (spw - 1)) : (t & (spw - 1)));
@@ -352,6 +353,7 @@ __global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, i
                                                       const double* side, size_t seg, double step, float norm_bw,
                                                       const float* st, float* out_base, size_t ostride, int* fail,
                                                       float2* rec, size_t rb, int inject) {
+    FMRX_RUNNER_PRIO();
     const int t = threadIdx.x & 63;
     const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int s_lane = wave * spw + (t & (spw - 1));
@@ -443,6 +445,7 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
                                                            float norm_bw, const float* st, float* out_base,
                                                            size_t ostride, int* fail, float2* rec, size_t rb,
                                                            int inject, int sat_ok, int pred_ok) {
+    FMRX_RUNNER_PRIO();
     const int t = threadIdx.x & 63;
     const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int s_lane = wave * spw + ((t >> 4) & (spw - 1));
@@ -741,12 +744,14 @@ __device__ inline AudioView view(const AudioLaunch& L, int s, int b) {
 
 constexpr int kTail = 64;  // mixer tail kept across calls (>= ceil((at-1)/up) + 1)
 
-__global__ void stereo_audio_kernel(AudioLaunch L) {
-    // grid.x = n_blocks x frame tiles (no 65,535 limit on the block count), grid.y = streams
+__global__ void stereo_audio_kernel(AudioLaunch L, int b0) {
+    // grid.x = blocks x frame tiles (no 65,535 limit on the block count), grid.y = streams;
+    // blocks b0, b0 + 1, ... of the call
     const int ft = (L.frames_per_block + (int)blockDim.x - 1) / (int)blockDim.x;
     const int s = blockIdx.y;
-    const int b = blockIdx.x / ft;
-    const int m = (blockIdx.x - b * ft) * blockDim.x + threadIdx.x;
+    const int bl = blockIdx.x / ft;
+    const int b = b0 + bl;
+    const int m = (blockIdx.x - bl * ft) * blockDim.x + threadIdx.x;
     if (m >= L.frames_per_block) return;
     const AudioView cur = view(L, s, b);
     const AudioView prv = b > 0 ? view(L, s, b - 1) : cur;
@@ -778,11 +783,11 @@ __global__ void stereo_audio_kernel(AudioLaunch L) {
 // delay line reads it back from LDS.  Same arithmetic as stereo_audio_kernel.
 constexpr int kTileIf = 1024, kTileFrames = 256, kTileTaps = 64;
 
-__global__ void __launch_bounds__(128) stereo_audio_tile_kernel(AudioLaunch L) {
+__global__ void __launch_bounds__(128) stereo_audio_tile_kernel(AudioLaunch L, int b0) {
     constexpr int kPer = kTileFrames / 128;    // frames per thread
     __shared__ float2 X[kTileTaps + kTileIf];  // X[H + j]: (mono input, stereo input) at IF index j
     __shared__ float C[kTileTaps], MO[kTileFrames];
-    const int s = blockIdx.y, b = blockIdx.x;
+    const int s = blockIdx.y, b = b0 + (int)blockIdx.x;  // block b of the call
     const int ipb = L.if_per_block, fpb = L.frames_per_block, at = L.at, H = at - 1;
     const AudioView cur = view(L, s, b);
     for (int i = threadIdx.x; i < ipb; i += blockDim.x) X[H + i] = make_float2(cur.d[i], mixer_at(cur, i));
@@ -987,13 +992,14 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     // the three-wave runner: every stream at the same known trigOffset t, a SIMD per wave (one
     // stream a workgroup of three); it takes the samples from trigOffset 2^20 on
     const bool pipe = spec && pred_ok && pipe_env && spw == 1 && 3 * n_streams <= n_simd && k && hlo == hhi;
-    // the index runner below 2^20 wants four SIMDs a stream (FMRX_PLL_IDX=0: not launched)
+    // the index runner in [2^18, 2^20) wants four SIMDs a stream (FMRX_PLL_IDX=0: not launched)
+    // (FMRX_PLL_IDX=2: also its 64-candidate form from 2^17)
     const int idx_env = [] {
         const char* e = std::getenv("FMRX_PLL_IDX");
-        return (e && e[0] == '0') ? 0 : 1;
+        return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
     }();
     const bool idx = pipe && idx_env && kPllIdxWaves * n_streams <= n_simd;
-    const double fast_min = idx ? (double)kPllIdxMin : (double)kPllPipeMinLow;
+    const double fast_min = idx ? (double)(idx_env == 2 ? kPllIdxMin64 : kPllIdxMin) : (double)kPllPipeMinLow;
     size_t n_seg = (size_t)n;  // samples through the segment loop
     if (pipe) n_seg = hlo >= fast_min ? 0 : std::min((size_t)n, (size_t)(fast_min - hlo));
 
@@ -1100,18 +1106,24 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     return ok();
 }
 
-int launch_stereo_audio(const AudioLaunch& L, int n_streams, hipStream_t s) {
-    if (L.n_blocks <= 0) return 0;
+int launch_stereo_audio_range(const AudioLaunch& L, int b0, int b1, bool last, int n_streams, hipStream_t s) {
+    if (L.n_blocks <= 0 || b0 < 0 || b1 > L.n_blocks || b0 > b1) return 0;
     const int H = L.at - 1;
-    if (L.up == 1 && L.if_per_block <= kTileIf && L.frames_per_block <= kTileFrames && L.at <= kTileTaps &&
-        L.frames_per_block * L.down <= L.if_per_block && (L.frames_per_block - kMonoDelay) * L.down >= H) {
-        hipLaunchKernelGGL(stereo_audio_tile_kernel, dim3(L.n_blocks, n_streams), dim3(128), 0, s, L);
-    } else {
-        const dim3 grid(((L.frames_per_block + 127) / 128) * L.n_blocks, n_streams);
-        hipLaunchKernelGGL(stereo_audio_kernel, grid, dim3(128), 0, s, L);
+    if (b1 > b0) {
+        if (L.up == 1 && L.if_per_block <= kTileIf && L.frames_per_block <= kTileFrames && L.at <= kTileTaps &&
+            L.frames_per_block * L.down <= L.if_per_block && (L.frames_per_block - kMonoDelay) * L.down >= H) {
+            hipLaunchKernelGGL(stereo_audio_tile_kernel, dim3(b1 - b0, n_streams), dim3(128), 0, s, L, b0);
+        } else {
+            const dim3 grid(((L.frames_per_block + 127) / 128) * (b1 - b0), n_streams);
+            hipLaunchKernelGGL(stereo_audio_kernel, grid, dim3(128), 0, s, L, b0);
+        }
     }
-    hipLaunchKernelGGL(stereo_state_kernel, dim3(n_streams), dim3(kTail), 0, s, L);
+    if (last) hipLaunchKernelGGL(stereo_state_kernel, dim3(n_streams), dim3(kTail), 0, s, L);
     return ok();
+}
+
+int launch_stereo_audio(const AudioLaunch& L, int n_streams, hipStream_t s) {
+    return launch_stereo_audio_range(L, 0, L.n_blocks, true, n_streams, s);
 }
 
 int launch_pll_fallback_test(int kind, const float* a, const float* b, size_t n, float* out, hipStream_t s) {

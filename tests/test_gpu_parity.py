@@ -481,6 +481,29 @@ def test_stereo_multistream(fmrx, orc):
         assert np.array_equal(out[s], orc.run(0, 51, iq, ["pcm"])["pcm"]), s
 
 
+@pytest.mark.parametrize("mode,n_streams,nb,chunks", [(0, 5, 48, "3"), (0, 1, 64, "4"), (1, 3, 40, "2"),
+                                                      (2, 2, 3, "2"), (0, 70, 120, None)])
+def test_stereo_pipelined_chunks(fmrx, orc, monkeypatch, mode, n_streams, nb, chunks):
+    """The pipelined stereo engine (api.cpp run_stereo_pipelined): a call's blocks in chunks,
+    front end + band-pass of chunk k + 1 and audio of chunk k - 1 on their own HIP streams beside
+    the PLL of chunk k, every chunk reading the call's buffers at its offset (a chunk's RF halo
+    is the call's own bytes in front of it).  FMRX_STEREO_CHUNKS forces the chunk count (None: the
+    default, 8 from 64 streams, fewer when a chunk would hold < 2^14 samples); two calls in a row
+    check the carried state.  Modes 0/1 take the tiled audio kernel, mode 2 the per-frame one."""
+    if chunks is not None:
+        monkeypatch.setenv("FMRX_STEREO_CHUNKS", chunks)
+    bb = oracle.MODES[mode][0]
+    rf_fs = oracle.MODES[mode][3]
+    recipes = [("synth:%d" if s % 3 else "rand:%d") % (500 + s) for s in range(n_streams)]
+    ins = np.stack([iqgen.make(r, 2 * nb * bb, rf_fs) for r in recipes])
+    with fmrx.Receiver(mode, fmrx.STEREO, n_streams=n_streams) as rx:
+        a = np.atleast_2d(rx.process(np.ascontiguousarray(ins[:, :nb * bb])))
+        b = np.atleast_2d(rx.process(np.ascontiguousarray(ins[:, nb * bb:])))
+    for s in sorted({0, n_streams // 2, n_streams - 1}):
+        want = orc.run(mode, 51, ins[s], ["pcm"])["pcm"]
+        assert np.array_equal(np.concatenate([a[s], b[s]]), want), s
+
+
 @pytest.mark.parametrize("channels,n_streams", [(2, 70), (1, 130), (2, 1100), (2, 4200)])
 def test_many_streams_cross_wave_boundaries(fmrx, orc, channels, n_streams):
     """Many streams of different content: the PLL runs one stream per wave until the streams
@@ -827,14 +850,15 @@ def test_pll_pipe_redo(fmrx, orc, monkeypatch, trig0, miss):
 
 @pytest.mark.parametrize("trig0", [131072.0, 262177.0, 524188.0, 600000.0, 1043576.0, 125000.0])
 @pytest.mark.parametrize("inject", [None, "5"])
-@pytest.mark.parametrize("idx", ["1", "0"])
+@pytest.mark.parametrize("idx", ["1", "0", "2"])
 def test_pll_index_runner(fmrx, orc, monkeypatch, trig0, inject, idx):
-    """trigOffset in [2^17, 2^20): the index runner (pll_pred.hip pll_idx_kernel: the chain forms
-    trigArg itself and reads its e from a lane of a 64-candidate row -- 64 candidates from 2^17,
-    32 from 2^18, 16 from 2^19), starting at 2^17, at 2^18 + 33, 100 steps below 2^19 (the 2^18
-    form hands over to the 2^19 one inside the call), at 600,000, and 5,000 steps below 2^20 (the
-    three-wave runner takes over); 125,000 starts on the lane runner and crosses into it.
-    FMRX_PLL_IDX=0: the lane runner below 2^20.  Bit-exact against the oracle; a forced miss
+    """trigOffset in [2^18, 2^20): the index runner (pll_pred.hip pll_idx_kernel: the chain forms
+    trigArg itself and reads its e from a lane of a candidate row -- 32 candidates from 2^18, 16
+    from 2^19; with FMRX_PLL_IDX=2 also 64 from 2^17), starting at 2^17 (the lane runner hands
+    over at 2^18), at 2^18 + 33, 100 steps below 2^19 (the 2^18 form hands over to the 2^19 one
+    inside the call), at 600,000, and 5,000 steps below 2^20 (the three-wave runner takes over);
+    125,000 starts on the lane runner and crosses into it.  FMRX_PLL_IDX=0: the lane runner below
+    2^20.  Bit-exact against the oracle; a forced miss
     (FMRX_PLL_SPEC_INJECT) is redone exactly, and without it no batch is."""
     monkeypatch.setenv("FMRX_PLL_IDX", idx)
     if inject is not None:

@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/gpu_dev.sh <tag> [steps...] — development GPU call: each named step under its own time
 # limit, stopping at the first failure.  Steps: tests (whole GPU suite), pll (PLL / stereo tests
-# only), n2 (the N=2 bench line rehearsed with gloo, both ranks on device 0), mfma (tools/ubench_mfma_add), testsall (whole GPU suite, not stopping at a failure), idx (the index-runner tests), ubench (tools/ubench_idx), stages (tools/stage_times.py), bench (bench.py, no CPU baseline), smoke.
+# only), n2 (the N=2 bench line rehearsed with gloo, both ranks on device 0), mfma (tools/ubench_mfma_add), prio (tools/overlap_probe.py with the product build and the s_setprio(3) runner build), predict (tools/pll_predict.cpp on a 72 s GPU-made carrier, lookback 2), rprof (tools/runner_prof.py per form, with the FMRX_AB_PROF build), testsall (whole GPU suite, not stopping at a failure), idx (the index-runner tests), ubench (tools/ubench_idx), stages (tools/stage_times.py), stages1 (configs[4] with the serial engine), pipe (the pipelined-engine tests), bench (bench.py, no CPU baseline), smoke.
 set -o pipefail
 TAG=${1:-dev}; shift
 OUT=gpurun_out/$TAG
@@ -23,12 +23,35 @@ for step in "$@"; do
            cat $OUT/ubench_mfma_add.txt ;;
     stages) timeout -k 10 300 python tools/stage_times.py > $OUT/stages.json 2> $OUT/stages.err || { tail $OUT/stages.err; exit 3; }
            cat $OUT/stages.json ;;
+    stages1) FMRX_STEREO_CHUNKS=1 timeout -k 10 300 python tools/stage_times.py --no-gib --single 0 > $OUT/stages_serial.json 2> $OUT/stages1.err || { tail $OUT/stages1.err; exit 3; }
+           cat $OUT/stages_serial.json ;;
+    pipe) timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread -k "pipelined or stereo_multistream or many_streams or bench_config or call_split" > $OUT/pipe.log 2>&1 || { tail -40 $OUT/pipe.log; exit 13; }
+           tail -2 $OUT/pipe.log ;;
     bench) timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 4; }
            python -c "import json; j=json.load(open('$OUT/bench.json')); print(j['value'], j['roofline']['kernel_ms'], json.dumps(j.get('baseline_configs',{}))[:1500])" ;;
     n2) FMRX_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
           --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 3 --no-cpu-baseline \
           > $OUT/bench_n2_gloo.json 2> $OUT/bench_n2_gloo.err || { tail $OUT/bench_n2_gloo.err; exit 9; }
           tail -c 3000 $OUT/bench_n2_gloo.json ;;
+    rprof) TR="262144 524288 1048576 2097152 4194304"
+           timeout -k 10 120 python tools/runner_prof.py --save /tmp/rp_states.npz $(for t in $TR; do echo --trig $t; done) \
+               > $OUT/runner_prof.txt 2>&1 || { tail $OUT/runner_prof.txt; exit 10; }
+           for tr in $TR; do
+             FMRX_LIB_PATH=software-defined-radio-course-project_amd/build_ab/libfmrx.so timeout -k 10 120 \
+               python tools/runner_prof.py --load /tmp/rp_states.npz --trig $tr >> $OUT/runner_prof.txt 2>&1 || { tail $OUT/runner_prof.txt; exit 10; }
+           done
+           timeout -k 10 120 python tools/runner_prof.py --load /tmp/rp_states.npz $(for t in $TR; do echo --trig $t; done) \
+               >> $OUT/runner_prof.txt 2>&1 || { tail $OUT/runner_prof.txt; exit 10; }
+           grep -v amdgpu.ids $OUT/runner_prof.txt ;;
+    predict) timeout -k 10 300 python tools/make_carrier.py /tmp/carrier.f32 72 > $OUT/predict.txt 2>&1 || { tail $OUT/predict.txt; exit 11; }
+             g++ -O2 -ffp-contract=off -o /tmp/pll_predict tools/pll_predict.cpp || exit 11
+             timeout -k 10 600 /tmp/pll_predict /tmp/carrier.f32 2 >> $OUT/predict.txt 2>&1 || { tail $OUT/predict.txt; exit 11; }
+             tail -40 $OUT/predict.txt ;;
+    prio) for lib in libfmrx.so build_prio/libfmrx.so; do
+            FMRX_LIB_PATH=software-defined-radio-course-project_amd/$lib timeout -k 10 300 python tools/overlap_probe.py \
+              >> $OUT/overlap_prio.json 2>> $OUT/overlap_prio.err || { tail $OUT/overlap_prio.err; exit 12; }
+          done
+          cat $OUT/overlap_prio.json ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail $OUT/smoke.log; exit 5; }
            tail -1 $OUT/smoke.log ;;
   esac

@@ -114,7 +114,7 @@ int main(int argc, char** argv) {
     for (int r = 2; r + 1 < 8; r++) {
         const size_t j0 = edges[r], j1 = std::min(edges[r + 1], N);
         if (j0 >= j1) continue;
-        for (int B : {8, 16}) {
+        for (int B : {8, 16, 32, 64}) {
             long hit = 0, nb_all = 0, nb_ok = 0;
             for (size_t b0 = (j0 / B) * B; b0 < j1; b0 += B) {
                 const size_t back = (size_t)(lb - 1) * B + 1;
