@@ -188,8 +188,9 @@ int reset_state(fmrx_ctx* c) {
     c->halo_cur = 0;
     HIPCHK(hipMemsetAsync(c->d_audio_hist.p, 0, sizeof(float) * c->audio_hist * ns, c->stream));
     c->audio_hist_stale = false;
-    if (c->d_demod.p)
-        HIPCHK(hipMemsetAsync(c->d_demod.p, 0, sizeof(float) * c->d_demod.n, c->stream));
+    if (c->d_demod.p)  // the history in front of each stream (every call overwrites the rest)
+        HIPCHK(hipMemset2DAsync(c->d_demod.p, c->demod_stride * sizeof(float), 0, sizeof(float) * kDemodHist, ns,
+                                c->stream));
     // project.cpp:106-111: integrator 0, phaseEst 0, feedbackI 1, feedbackQ 0,
     // ncoOut_state 1, trigOffset 0
     std::vector<float> pll(8 * ns, 0.0f);
@@ -269,9 +270,11 @@ int run_rds(fmrx_ctx* c, const float* d_demod, size_t demod_stride, size_t n_if,
 // Segments per stream for the fused kernel: enough workgroups to fill the chip
 // (2 resident per CU on 256 CUs) without making segments so short that the pre-roll chunk
 // dominates.
-int mono_segments(const fmrx_ctx* c, long long n_if) {
+int mono_segments(const fmrx_ctx* c, long long n_if, int wg_per_cu = 0) {
     const long long chunks = mono_chunks(n_if, c->geo.rf_taps, c->geo.rf_decim, c->geo.audio_down);
-    const long long target_wg = 256LL * mono_wg_per_cu(c->geo.rf_decim);  // one full wave of workgroups
+    // one full wave of workgroups (or wg_per_cu a CU: the pipelined stereo front end, which
+    // leaves the rest of each CU's LDS and SIMDs to the PLL runners beside it)
+    const long long target_wg = 256LL * (wg_per_cu > 0 ? wg_per_cu : mono_wg_per_cu(c->geo.rf_decim));
     long long segs = std::max<long long>(1, target_wg / std::max(1, c->cfg.n_streams));
     segs = std::min(segs, std::max<long long>(1, chunks / 4));
     return (int)std::max<long long>(1, segs);
@@ -293,6 +296,11 @@ int mono_older_share(const fmrx_ctx* c, int segs) {
         return 0;
     return share;
 }
+
+// Workgroups a CU of the pipelined stereo front end (two of the fused kernel's 18.8 KB and one
+// wave each): a full grid (8 a CU) holds every CU's LDS for its whole span, and a PLL launch
+// queued behind it on the context stream waits until it drains.
+constexpr int kPipeFrontWgPerCu = 2;
 
 // RF front end (+ the mono audio stage when `pcm` is non-null and the mode allows it).
 // Chunk form (the stereo pipeline, run_stereo_pipelined): blocks [b0, b0 + n_blocks) of a call of
@@ -326,7 +334,7 @@ int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
     L.stream_bytes = n_blocks * c->geo.block_bytes;
     L.halo_bytes = c->halo_bytes;
     L.n_if = (long long)(n_blocks * c->geo.if_samples);
-    L.segs = mono_segments(c, L.n_if);
+    L.segs = mono_segments(c, L.n_if, call_blocks != n_blocks ? kPipeFrontWgPerCu : 0);
     L.older_share = mono_older_share(c, L.segs);
     L.stamps = c->stamps;
     L.audio = with_audio ? 1 : 0;
@@ -459,10 +467,15 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
 // samples a stream, so a call pipelines when it has many streams and enough blocks a chunk.
 // FMRX_STEREO_CHUNKS=k forces k chunks (1: the serial engine).
 int stereo_chunks(const fmrx_ctx* c, size_t n_blocks) {
-    if (const char* e = std::getenv("FMRX_STEREO_CHUNKS"))  // at least a block a chunk
-        return (int)std::min<size_t>((size_t)std::max(1, std::atoi(e)), std::max<size_t>(n_blocks, 1));
     int k = c->cfg.n_streams >= 64 ? 8 : 1;
-    while (k > 1 && n_blocks * c->geo.if_samples / (size_t)k < 16384) k--;  // >= 2^14 samples a chunk
+    const char* e = std::getenv("FMRX_STEREO_CHUNKS");
+    if (e) k = std::max(1, std::atoi(e));
+    else
+        while (k > 1 && n_blocks * c->geo.if_samples / (size_t)k < 16384) k--;  // >= 2^14 samples a chunk
+    // a chunk past the first reads its RF halo from the call's own bytes in front of it: every
+    // chunk holds at least the halo's blocks
+    const size_t hb = (c->halo_bytes + c->geo.block_bytes - 1) / c->geo.block_bytes;
+    while (k > 1 && n_blocks / (size_t)k < hb) k--;
     return k;
 }
 
@@ -477,13 +490,15 @@ int stereo_chunks(const fmrx_ctx* c, size_t n_blocks) {
 int run_stereo_pipelined(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm, float* d_mono, int K) {
     const int ns = c->cfg.n_streams;
     const size_t ipb = c->geo.if_samples, n_if = n_blocks * ipb;
-    if (c->halo_bytes > c->geo.block_bytes) return fail(FMRX_EINVAL, "halo larger than a block");
+    if (n_blocks / (size_t)K * c->geo.block_bytes < c->halo_bytes) return fail(FMRX_EINVAL, "chunks shorter than the halo");
     int rc = c->d_channel.ensure(n_if * ns);
     if (!rc) rc = c->d_carrier.ensure(n_if * ns);
     if (rc) return rc;
-    if (!c->s_front) {
-        HIPCHK(hipStreamCreateWithFlags(&c->s_front, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&c->s_audio, hipStreamNonBlocking));
+    if (!c->s_front) {  // the lowest priority: the PLL's launches go first when a CU frees up
+        int lo = 0, hi = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(hipStreamCreateWithPriority(&c->s_front, hipStreamNonBlocking, lo));
+        HIPCHK(hipStreamCreateWithPriority(&c->s_audio, hipStreamNonBlocking, lo));
     }
     const size_t n_ev = 2 * (size_t)K + 2;
     while (c->pipe_ev.size() < n_ev) {
@@ -691,7 +706,11 @@ int fmrx_create(const fmrx_config* cfg, fmrx_ctx** out) {
 
     const int ns = cfg->n_streams;
     auto cleanup = [&](int code) { fmrx_destroy(c); return code; };
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    // the context stream at the highest priority (the serial PLL of the pipelined stereo engine
+    // runs on it, its stage streams at the lowest)
+    int prio_lo = 0, prio_hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess)
         return cleanup(fail(FMRX_EHIP, "hipStreamCreate failed"));
     c->halo_bytes = mono_halo_bytes(g.rf_taps, g.rf_decim, g.audio_down);
     c->audio_hist = g.audio_taps_total - 1;

@@ -49,6 +49,9 @@ namespace fmrx {
 __device__ unsigned long long g_pred_prof[6];
 __device__ unsigned long long g_pipe_prof[6];
 __device__ unsigned long long g_idx_prof[6];
+// redos per stream (blockIdx.x) and form: pipe 16-step, pipe 64-step five, pipe three, index
+constexpr int kProfStreams = 4096;
+__device__ unsigned int g_redo_stream[4][kProfStreams];
 #define PROF_T() __builtin_amdgcn_s_memtime()
 #else
 #define PROF_T() 0ull
@@ -999,6 +1002,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         atomicAdd(&g_pipe_prof[1], ch_wait);
         atomicAdd(&g_pipe_prof[4], (unsigned long long)ni);
         atomicAdd(&g_pipe_prof[5], n_redo);
+        if (s < kProfStreams) atomicAdd(&g_redo_stream[NI == 16 ? 0 : NC == 5 ? 1 : 2][s], (unsigned int)n_redo);
     }
 #endif
     (void)ch_body;
@@ -1269,6 +1273,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         atomicAdd(&g_idx_prof[1], ch_wait);
         atomicAdd(&g_idx_prof[4], (unsigned long long)ni);
         atomicAdd(&g_idx_prof[5], n_redo);
+        if (s < kProfStreams) atomicAdd(&g_redo_stream[3][s], (unsigned int)n_redo);
     }
 #endif
     (void)ch_body;
@@ -1308,6 +1313,23 @@ static void print_pred_prof() {
         std::fprintf(stderr, "pll_idx prof: intervals %llu chain body %.1f wait %.1f, evaluator body %.1f wait %.1f "
                      "(shader cycles per interval), %llu redos\n", h[4], (double)h[0] / h[4], (double)h[1] / h[4],
                      (double)h[2] / h[4], (double)h[3] / h[4], h[5]);
+    static unsigned int rs[4][kProfStreams];
+    if (hipMemcpyFromSymbol(rs, HIP_SYMBOL(g_redo_stream), sizeof rs) == hipSuccess) {
+        const char* names[4] = {"pipe 16-step", "pipe 64-step five", "pipe three", "index"};
+        for (int f = 0; f < 4; f++) {
+            unsigned long long tot = 0;
+            unsigned int mx = 0;
+            int n = 0, arg = -1;
+            for (int k = 0; k < kProfStreams; k++) {
+                tot += rs[f][k];
+                if (rs[f][k]) n++;
+                if (rs[f][k] > mx) { mx = rs[f][k]; arg = k; }
+            }
+            if (tot)
+                std::fprintf(stderr, "redos per stream, %s: total %llu over %d streams, max %u (stream %d)\n", names[f],
+                             tot, n, mx, arg);
+        }
+    }
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pipe_prof), sizeof h) == hipSuccess && h[4])
         std::fprintf(stderr, "pll_pipe prof: intervals %llu chain body %.1f wait %.1f, evaluator body %.1f wait %.1f "
                      "(shader cycles per interval), %llu redos\n", h[4], (double)h[0] / h[4], (double)h[1] / h[4],
