@@ -297,9 +297,10 @@ int mono_older_share(const fmrx_ctx* c, int segs) {
     return share;
 }
 
-// Workgroups a CU of the pipelined stereo front end (two of the fused kernel's 18.8 KB and one
-// wave each): a full grid (8 a CU) holds every CU's LDS for its whole span, and a PLL launch
-// queued behind it on the context stream waits until it drains.
+// Workgroups a CU of the pipelined stereo front end past the first chunk (two of the fused
+// kernel's 18.8 KB and one wave each): a full grid (8 a CU) holds every CU's LDS for its whole
+// span, and a PLL launch queued behind it on the context stream waits until it drains.  The first
+// chunk's front end runs alone (full grid).
 constexpr int kPipeFrontWgPerCu = 2;
 
 // RF front end (+ the mono audio stage when `pcm` is non-null and the mode allows it).
@@ -334,7 +335,7 @@ int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
     L.stream_bytes = n_blocks * c->geo.block_bytes;
     L.halo_bytes = c->halo_bytes;
     L.n_if = (long long)(n_blocks * c->geo.if_samples);
-    L.segs = mono_segments(c, L.n_if, call_blocks != n_blocks ? kPipeFrontWgPerCu : 0);
+    L.segs = mono_segments(c, L.n_if, b0 > 0 ? kPipeFrontWgPerCu : 0);
     L.older_share = mono_older_share(c, L.segs);
     L.stamps = c->stamps;
     L.audio = with_audio ? 1 : 0;
@@ -475,8 +476,17 @@ int stereo_chunks(const fmrx_ctx* c, size_t n_blocks) {
     // a chunk past the first reads its RF halo from the call's own bytes in front of it: every
     // chunk holds at least the halo's blocks
     const size_t hb = (c->halo_bytes + c->geo.block_bytes - 1) / c->geo.block_bytes;
-    while (k > 1 && n_blocks / (size_t)k < hb) k--;
+    while (k > 1 && n_blocks / (2 * (size_t)(k - 1)) < hb) k--;  // the half-size end chunks too
     return k;
+}
+
+// First block of chunk k of K (k = K: n_blocks).  The first and the last chunk are half the
+// others: the first chunk's front end and the last chunk's NCO and audio stage have no PLL
+// beside them.
+size_t chunk_begin(size_t n_blocks, int k, int K) {
+    if (K <= 1 || k <= 0) return k <= 0 ? 0 : n_blocks;
+    if (k >= K) return n_blocks;
+    return (size_t)(((unsigned long long)n_blocks * (unsigned long long)(2 * k - 1)) / (2ULL * (K - 1)));
 }
 
 // The stereo engine over the call's blocks in K chunks, pipelined like project.cpp's two threads
@@ -490,7 +500,9 @@ int stereo_chunks(const fmrx_ctx* c, size_t n_blocks) {
 int run_stereo_pipelined(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm, float* d_mono, int K) {
     const int ns = c->cfg.n_streams;
     const size_t ipb = c->geo.if_samples, n_if = n_blocks * ipb;
-    if (n_blocks / (size_t)K * c->geo.block_bytes < c->halo_bytes) return fail(FMRX_EINVAL, "chunks shorter than the halo");
+    for (int k = 0; k < K; k++)
+        if ((chunk_begin(n_blocks, k + 1, K) - chunk_begin(n_blocks, k, K)) * c->geo.block_bytes < c->halo_bytes)
+            return fail(FMRX_EINVAL, "chunks shorter than the halo");
     int rc = c->d_channel.ensure(n_if * ns);
     if (!rc) rc = c->d_carrier.ensure(n_if * ns);
     if (rc) return rc;
@@ -500,20 +512,23 @@ int run_stereo_pipelined(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int1
         HIPCHK(hipStreamCreateWithPriority(&c->s_front, hipStreamNonBlocking, lo));
         HIPCHK(hipStreamCreateWithPriority(&c->s_audio, hipStreamNonBlocking, lo));
     }
-    const size_t n_ev = 2 * (size_t)K + 2;
+    const size_t n_ev = 2 * (size_t)K + 3;
     while (c->pipe_ev.size() < n_ev) {
         hipEvent_t e;
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         c->pipe_ev.push_back(e);
     }
-    hipEvent_t ev_start = c->pipe_ev[0], ev_end = c->pipe_ev[1];
+    hipEvent_t ev_start = c->pipe_ev[0], ev_end = c->pipe_ev[1], ev_lane = c->pipe_ev[2 * (size_t)K + 2];
     auto ev_bp = [&](int k) { return c->pipe_ev[2 + 2 * (size_t)k]; };
     auto ev_pll = [&](int k) { return c->pipe_ev[3 + 2 * (size_t)k]; };
     // both side streams start after everything enqueued on the context stream so far
     HIPCHK(hipEventRecord(ev_start, c->stream));
     HIPCHK(hipStreamWaitEvent(c->s_front, ev_start, 0));
     HIPCHK(hipStreamWaitEvent(c->s_audio, ev_start, 0));
-    if ((rc = c->d_pll_side.ensure(pll_side_doubles((int)((n_blocks + K - 1) / K * ipb), ns)))) return rc;
+    size_t max_m = 0;
+    for (int k = 0; k < K; k++)
+        max_m = std::max(max_m, (chunk_begin(n_blocks, k + 1, K) - chunk_begin(n_blocks, k, K)) * ipb);
+    if ((rc = c->d_pll_side.ensure(pll_side_doubles((int)max_m, ns)))) return rc;
     AudioLaunch A{};
     A.demod = c->d_demod.p;
     A.demod_stride = c->demod_stride;
@@ -531,10 +546,27 @@ int run_stereo_pipelined(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int1
     A.down = c->geo.audio_down;
     A.at = c->geo.audio_taps_total;
     A.audio_c = c->d_audio.p;
+    // the PLL of chunk 0 in two launches when its streams start below the index runner's range:
+    // the lane runner's segments first (issue-bound: a front-end wave sharing its SIMD halves its
+    // rate), then the rest; chunk 1's front end waits for the first part
+    size_t lane_m = 0;
+    if (c->pll_trig.known && c->pll_trig.lo == c->pll_trig.hi && c->pll_trig.lo < (double)kPllIdxMin)
+        lane_m = (size_t)((double)kPllIdxMin - c->pll_trig.lo);
+    auto pll = [&](size_t off, size_t m) -> int {
+        if (m == 0) return 0;
+        if (launch_pll(c->d_carrier.p + off, (int)m, ns, n_if, 19000.0f, (float)c->geo.if_fs, 2.0f, 0.0f, 0.01f,
+                       c->d_pll.p, c->d_pll_side.p, c->stream, c->hint(c->pll_trig), c->pll_stats)) {
+            c->pll_trig.known = false;
+            return fail(FMRX_EHIP, "PLL launch failed");
+        }
+        c->pll_trig.advance(m);
+        return 0;
+    };
     for (int k = 0; k < K; k++) {
-        const size_t b0 = n_blocks * (size_t)k / K, b1 = n_blocks * (size_t)(k + 1) / K;
+        const size_t b0 = chunk_begin(n_blocks, k, K), b1 = chunk_begin(n_blocks, k + 1, K);
         const size_t nb = b1 - b0, m = nb * ipb, off = b0 * ipb;
         const bool last = k == K - 1;
+        if (k == 1 && lane_m > 0) HIPCHK(hipStreamWaitEvent(c->s_front, ev_lane, 0));
         // s_front: front end and band-pass pair of chunk k
         if ((rc = run_fused(c, d_iq, nb, nullptr, nullptr, c->d_demod.p, c->demod_stride, kDemodHist, false, b0,
                             n_blocks, c->s_front, last)))
@@ -556,12 +588,10 @@ int run_stereo_pipelined(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int1
         HIPCHK(hipEventRecord(ev_bp(k), c->s_front));
         // the context stream: the PLL of chunk k (project.cpp:166)
         HIPCHK(hipStreamWaitEvent(c->stream, ev_bp(k), 0));
-        if (launch_pll(c->d_carrier.p + off, (int)m, ns, n_if, 19000.0f, (float)c->geo.if_fs, 2.0f, 0.0f, 0.01f,
-                       c->d_pll.p, c->d_pll_side.p, c->stream, c->hint(c->pll_trig), c->pll_stats)) {
-            c->pll_trig.known = false;
-            return fail(FMRX_EHIP, "PLL launch failed");
-        }
-        c->pll_trig.advance(m);
+        const size_t m0 = k == 0 ? std::min(lane_m, m) : 0;
+        if ((rc = pll(off, m0))) return rc;
+        if (k == 0 && lane_m > 0) HIPCHK(hipEventRecord(ev_lane, c->stream));
+        if ((rc = pll(off + m0, m - m0))) return rc;
         HIPCHK(hipEventRecord(ev_pll(k), c->stream));
         // s_audio: the audio stage of chunk k (and the state carry after the last)
         HIPCHK(hipStreamWaitEvent(c->s_audio, ev_pll(k), 0));

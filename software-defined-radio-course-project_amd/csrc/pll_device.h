@@ -12,14 +12,6 @@
 namespace fmrx {
 namespace {
 
-// A/B experiment (Makefile `ab`, AB=-DFMRX_AB_PRIO): the serial PLL runners' waves at the highest
-// issue priority, so parallel kernels sharing their SIMDs take only the issue slots they leave
-#ifdef FMRX_AB_PRIO
-#define FMRX_RUNNER_PRIO() __builtin_amdgcn_s_setprio(3)
-#else
-#define FMRX_RUNNER_PRIO() ((void)0)
-#endif
-
 // src/filter.cpp:136-174 PLL.  A nonlinear recurrence: strictly serial in time, so one lane
 // per stream.  Float state; the reference's double atan2 / cos / sin results rounded to
 // float come from pll_math.h's certified fast path (fallback: the full library call).
@@ -72,6 +64,52 @@ __device__ __noinline__ PllPair pll_redo(PllState p, PllCtx ctx, const float* xb
     for (int j = 0; j < n; j++) {
         const float a = pll_step(p, ctx, xb[j], Ki, Kp, step, lib);
         if (wr) ob[j] = a;
+    }
+    return PllPair{p, ctx};
+}
+
+// The same steps, bit for bit, in batches of 16 on the certified fast path where it certifies
+// (pll_batch_fast, ~2.5x cheaper than 16 pll_step: pll_check_kernel's recipe -- 1/v as a
+// reciprocal with one Newton step, P = step x trigOffset as pll_side forms it), pll_step for a
+// batch that does not certify, for the steps before the context is valid and for the rest.  For
+// the self-certifying runners' redo of a missed interval (pll_pred.hip), whose state is always in
+// the trigOffset domain.
+__device__ __noinline__ PllPair pll_redo_fast(PllState p, PllCtx ctx, const float* xb, float* ob, int n, float Ki,
+                                              float Kp, double step) {
+    constexpr int NB = 16;
+    const DeviceLib lib;
+    int j = 0;
+#pragma unroll 1
+    while (j < n) {
+        const double t0d = (double)p.trig;
+        const bool fast = ctx.valid && j + NB <= n && pll_trig_domain(p.trig) &&
+                          fabs(step * fmin(t0d + (double)NB, (double)kPllTrigStick)) < kPllMaxPr;
+        if (fast) {
+            float v[NB], c[NB];
+            double iv[NB], pr[NB];
+#pragma unroll
+            for (int k = 0; k < NB; k++) {
+                v[k] = xb[j + k];
+                const double vd = (double)v[k];
+                const double r0 = __builtin_amdgcn_rcp(vd);
+                const double r1 = fma(r0, fma(-vd, r0, 1.0), r0);
+                iv[k] = (fabs(vd) >= (double)kPllMinV && fabs(vd) < 1.0e300) ? r1 : (double)NAN;
+                pr[k] = step * fmin(t0d + (double)(k + 1), (double)kPllTrigStick);
+            }
+            PllState q = p;
+            PllCtx cq = ctx;
+            if (pll_batch_fast<NB, false>(q, cq, v, iv, pr, c, Ki, Kp, [](int) {})) {
+#pragma unroll
+                for (int k = 0; k < NB; k++) ob[j + k] = c[k];
+                p = q;
+                ctx = cq;
+                j += NB;
+                continue;
+            }
+        }
+        const int e = fast ? j + NB : j + 1;  // a batch that did not certify, or one step
+#pragma unroll 1
+        for (; j < e; j++) ob[j] = pll_step(p, ctx, xb[j], Ki, Kp, step, lib);
     }
     return PllPair{p, ctx};
 }

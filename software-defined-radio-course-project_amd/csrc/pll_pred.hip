@@ -56,6 +56,13 @@ __device__ unsigned int g_redo_stream[4][kProfStreams];
 #else
 #define PROF_T() 0ull
 #endif
+// the self-certifying runners' exact redo of a missed interval: in certified 16-step batches
+// (pll_redo_fast), or (A/B build, AB=-DFMRX_REDO_PLAIN) step by step
+#ifdef FMRX_REDO_PLAIN
+#define FMRX_REDO(q, c, xb, ob, n, Ki, Kp, step) pll_redo(q, c, xb, ob, n, Ki, Kp, step, true)
+#else
+#define FMRX_REDO(q, c, xb, ob, n, Ki, Kp, step) pll_redo_fast(q, c, xb, ob, n, Ki, Kp, step)
+#endif
 
 namespace {
 
@@ -218,7 +225,6 @@ __global__ void __launch_bounds__(128) pll_pred_kernel(const float* io, int n, i
                                                       const float* st, float* out_base, size_t ostride, int* fail,
                                                       float2* rec, size_t rb, int inject, int sat_ok,
                                                       int pipe_on) {
-    FMRX_RUNNER_PRIO();
     // per step of the batch, double-buffered by batch parity: the phase thresholds of c0 and
     // c0 + 1 ulp, the bits of c0 - 1 ulp and the next step's e for c0 - 1 ulp (sa); its e for c0
     // and c0 + 1 ulp and P (sb: e_0, e_p, P as two words).  Two 16-B reads a step: the chain
@@ -575,7 +581,6 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                                                       double step, float norm_bw, float* st, float* out_base,
                                                       size_t ostride, int inject, int miss,
                                                       unsigned long long* stats) {
-    FMRX_RUNNER_PRIO();
     constexpr int NI = NB * BPI;
     static_assert(NI == 16 || NI == 32 || NI == 64, "the evaluators' lane map: 64 / NI lanes a step");
     static_assert(NC == 3 || NC == 5, "three or five candidates");
@@ -635,7 +640,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     // steps [j0, j1) exactly from state q (c): outputs
     auto exact = [&](PllState& q, PllCtx& c, long long j0, long long j1) {
         if (j1 > j0) {
-            const PllPair z = pll_redo(q, c, x + j0, out + j0, (int)(j1 - j0), Ki, Kp, step, true);
+            const PllPair z = FMRX_REDO(q, c, x + j0, out + j0, (int)(j1 - j0), Ki, Kp, step);
             q = z.p;
             c = z.ctx;
         }
@@ -1043,7 +1048,6 @@ template <int NC, int NW>
 __global__ void __launch_bounds__(64 * (1 + NW)) __attribute__((amdgpu_waves_per_eu(1, 1)))
 pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step, float norm_bw, float* st,
                float* out_base, size_t ostride, int inject, int miss, float lo, float hi, unsigned long long* stats) {
-    FMRX_RUNNER_PRIO();
     constexpr int NI = 16;          // steps an interval
     constexpr int SPP = 64 / NC;    // steps a candidate row
     constexpr int NR = NI / SPP;    // candidate rows an interval
@@ -1080,7 +1084,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
     const int inj = inject >= 0 && ni > 0 ? 1 + (inject + s) % ni : -1;
     auto exact = [&](PllState& q, PllCtx& c, long long j0, long long j1) {
         if (j1 > j0) {
-            const PllPair z = pll_redo(q, c, x + j0, out + j0, (int)(j1 - j0), Ki, Kp, step, true);
+            const PllPair z = FMRX_REDO(q, c, x + j0, out + j0, (int)(j1 - j0), Ki, Kp, step);
             q = z.p;
             c = z.ctx;
         }

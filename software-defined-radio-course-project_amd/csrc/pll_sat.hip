@@ -36,7 +36,6 @@ __global__ void __launch_bounds__(256) pll_sat_kernel(const float* io, int n, in
                                                      const double* side, size_t seg, double step, float norm_bw,
                                                      const float* st, float* out_base, size_t ostride, int* fail,
                                                      float2* rec, size_t rb, int inject) {
-    FMRX_RUNNER_PRIO();
     const int t = threadIdx.x & 63;
     const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int s_lane = wave * spw + ((t >> 4) & (spw - 1));

@@ -229,7 +229,6 @@ __global__ void __launch_bounds__(256) pll_kernel(float* io, int n, int n_stream
                                                  const double* side, size_t seg, double step, float norm_bw,
                                                  float* st, float* out_base, size_t ostride, const int* fail,
                                                  const float2* rec, size_t rb, unsigned long long* stats) {
-    FMRX_RUNNER_PRIO();
     const int t = threadIdx.x & 63;
     const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int s_lane = wave * spw + (SPLIT ? ((t >> 4) & (spw - 1)) : (t & (spw - 1)));
@@ -353,7 +352,6 @@ __global__ void __launch_bounds__(256) pll_spec_kernel(const float* io, int n, i
                                                       const double* side, size_t seg, double step, float norm_bw,
                                                       const float* st, float* out_base, size_t ostride, int* fail,
                                                       float2* rec, size_t rb, int inject) {
-    FMRX_RUNNER_PRIO();
     const int t = threadIdx.x & 63;
     const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int s_lane = wave * spw + (t & (spw - 1));
@@ -445,7 +443,6 @@ __global__ void __launch_bounds__(256) pll_spec_lane_kernel(const float* io, int
                                                            float norm_bw, const float* st, float* out_base,
                                                            size_t ostride, int* fail, float2* rec, size_t rb,
                                                            int inject, int sat_ok, int pred_ok) {
-    FMRX_RUNNER_PRIO();
     const int t = threadIdx.x & 63;
     const int wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int s_lane = wave * spw + ((t >> 4) & (spw - 1));
