@@ -68,52 +68,6 @@ __device__ __noinline__ PllPair pll_redo(PllState p, PllCtx ctx, const float* xb
     return PllPair{p, ctx};
 }
 
-// The same steps, bit for bit, in batches of 16 on the certified fast path where it certifies
-// (pll_batch_fast, ~2.5x cheaper than 16 pll_step: pll_check_kernel's recipe -- 1/v as a
-// reciprocal with one Newton step, P = step x trigOffset as pll_side forms it), pll_step for a
-// batch that does not certify, for the steps before the context is valid and for the rest.  For
-// the self-certifying runners' redo of a missed interval (pll_pred.hip), whose state is always in
-// the trigOffset domain.
-__device__ __noinline__ PllPair pll_redo_fast(PllState p, PllCtx ctx, const float* xb, float* ob, int n, float Ki,
-                                              float Kp, double step) {
-    constexpr int NB = 16;
-    const DeviceLib lib;
-    int j = 0;
-#pragma unroll 1
-    while (j < n) {
-        const double t0d = (double)p.trig;
-        const bool fast = ctx.valid && j + NB <= n && pll_trig_domain(p.trig) &&
-                          fabs(step * fmin(t0d + (double)NB, (double)kPllTrigStick)) < kPllMaxPr;
-        if (fast) {
-            float v[NB], c[NB];
-            double iv[NB], pr[NB];
-#pragma unroll
-            for (int k = 0; k < NB; k++) {
-                v[k] = xb[j + k];
-                const double vd = (double)v[k];
-                const double r0 = __builtin_amdgcn_rcp(vd);
-                const double r1 = fma(r0, fma(-vd, r0, 1.0), r0);
-                iv[k] = (fabs(vd) >= (double)kPllMinV && fabs(vd) < 1.0e300) ? r1 : (double)NAN;
-                pr[k] = step * fmin(t0d + (double)(k + 1), (double)kPllTrigStick);
-            }
-            PllState q = p;
-            PllCtx cq = ctx;
-            if (pll_batch_fast<NB, false>(q, cq, v, iv, pr, c, Ki, Kp, [](int) {})) {
-#pragma unroll
-                for (int k = 0; k < NB; k++) ob[j + k] = c[k];
-                p = q;
-                ctx = cq;
-                j += NB;
-                continue;
-            }
-        }
-        const int e = fast ? j + NB : j + 1;  // a batch that did not certify, or one step
-#pragma unroll 1
-        for (; j < e; j++) ob[j] = pll_step(p, ctx, xb[j], Ki, Kp, step, lib);
-    }
-    return PllPair{p, ctx};
-}
-
 // NB samples per optimistic batch.  Measured (10 s mode-0 stereo): NB = 16 beats 8 and 12.  The
 // certification is ~23 % of the step: without it the loop runs 0.31 s instead of 0.40 s.
 constexpr int kPllBatch = 16;

@@ -56,13 +56,6 @@ __device__ unsigned int g_redo_stream[4][kProfStreams];
 #else
 #define PROF_T() 0ull
 #endif
-// the self-certifying runners' exact redo of a missed interval: in certified 16-step batches
-// (pll_redo_fast), or (A/B build, AB=-DFMRX_REDO_PLAIN) step by step
-#ifdef FMRX_REDO_PLAIN
-#define FMRX_REDO(q, c, xb, ob, n, Ki, Kp, step) pll_redo(q, c, xb, ob, n, Ki, Kp, step, true)
-#else
-#define FMRX_REDO(q, c, xb, ob, n, Ki, Kp, step) pll_redo_fast(q, c, xb, ob, n, Ki, Kp, step)
-#endif
 
 namespace {
 
@@ -640,7 +633,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     // steps [j0, j1) exactly from state q (c): outputs
     auto exact = [&](PllState& q, PllCtx& c, long long j0, long long j1) {
         if (j1 > j0) {
-            const PllPair z = FMRX_REDO(q, c, x + j0, out + j0, (int)(j1 - j0), Ki, Kp, step);
+            const PllPair z = pll_redo(q, c, x + j0, out + j0, (int)(j1 - j0), Ki, Kp, step, true);
             q = z.p;
             c = z.ctx;
         }
@@ -1084,7 +1077,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
     const int inj = inject >= 0 && ni > 0 ? 1 + (inject + s) % ni : -1;
     auto exact = [&](PllState& q, PllCtx& c, long long j0, long long j1) {
         if (j1 > j0) {
-            const PllPair z = FMRX_REDO(q, c, x + j0, out + j0, (int)(j1 - j0), Ki, Kp, step);
+            const PllPair z = pll_redo(q, c, x + j0, out + j0, (int)(j1 - j0), Ki, Kp, step, true);
             q = z.p;
             c = z.ctx;
         }
