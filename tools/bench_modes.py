@@ -14,7 +14,6 @@ import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tests"))
-sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 
 def main():

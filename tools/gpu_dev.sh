@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/gpu_dev.sh <tag> [steps...] — development GPU call: each named step under its own time
 # limit, stopping at the first failure.  Steps: tests (whole GPU suite), pll (PLL / stereo tests
-# only), n2 (the N=2 bench line rehearsed with gloo, both ranks on device 0), mfma (tools/ubench_mfma_add), predict (tools/pll_predict.cpp on a 72 s GPU-made carrier, lookback 2), rprof (tools/runner_prof.py per form, with the FMRX_AB_PROF build), testsall (whole GPU suite, not stopping at a failure), idx (the index-runner tests), ubench (tools/ubench_idx), stages (tools/stage_times.py), stages1 (configs[4] with the serial engine), pipe (the pipelined-engine tests), redoc4 (configs[4] with the FMRX_AB_PROF build: runner cycles and redos per stream), ktrace (kernel trace of configs[4] calls + tools/trace_overlap.py), bench (bench.py, no CPU baseline), smoke.
+# only), n2 (the N=2 bench line rehearsed with gloo, both ranks on device 0), mfma (tools/ubench_mfma_add), predict (tools/pll_predict.cpp on a 72 s GPU-made carrier, lookback 2), rprof (tools/runner_prof.py per form, with the FMRX_AB_PROF build), testsall (whole GPU suite, not stopping at a failure), idx (the index-runner tests), ubench (tools/ubench_idx), stages (tools/stage_times.py), stages1 (configs[4] with the serial engine), pipe (the pipelined-engine tests), libab (stage_times per A/B build in $LIBS, alternating, twice), redoc4 (configs[4] with the FMRX_AB_PROF build: runner cycles and redos per stream), ktrace (kernel trace of configs[4] calls + tools/trace_overlap.py), bench (bench.py, no CPU baseline), smoke.
 set -o pipefail
 TAG=${1:-dev}; shift
 OUT=gpurun_out/$TAG
@@ -54,6 +54,13 @@ for step in "$@"; do
     redoc4) FMRX_LIB_PATH=software-defined-radio-course-project_amd/build_ab/libfmrx.so timeout -k 10 300 \
               python tools/stage_times.py --no-gib --single 0 > $OUT/redo_c4.json 2> $OUT/redo_c4.err || { tail $OUT/redo_c4.err; exit 15; }
             grep -v amdgpu.ids $OUT/redo_c4.err ;;
+    libab) # stage_times with each A/B build named in $LIBS (package-relative .so paths), alternating, twice
+            for r in 1 2; do for lib in ${LIBS:-libfmrx.so}; do
+              tagl=$(echo $lib | tr / _)
+              FMRX_LIB_PATH=software-defined-radio-course-project_amd/$lib timeout -k 10 300 python tools/stage_times.py \
+                > $OUT/libab_${r}_$tagl.json 2>> $OUT/libab.err || { tail $OUT/libab.err; exit 16; }
+              echo "$r $lib $(python -c "import json,sys; j=json.load(open(sys.argv[1])); print({k: v['wall_s'] for k, v in j.items()})" $OUT/libab_${r}_$tagl.json)"
+            done; done ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail $OUT/smoke.log; exit 5; }
            tail -1 $OUT/smoke.log ;;
   esac
