@@ -111,6 +111,8 @@ struct fmrx_ctx {
     DevBuf<float> d_f32;
     DevBuf<float> d_scratch;
     DevBuf<double> d_pll_side;    // PLL side data of one segment (pll_side_doubles)
+    DevBuf<double> d_pll_side2;   // the pipelined engine's second one (odd chunks: their NCO runs
+                                  //   on the audio stream while the next chunk's PLL fills the first)
     DevBuf<int16_t> d_sintab;
     DevBuf<uint8_t> d_synth_params;  // fmrx_synth_device_streams: SynthParams per stream
     // kernel timing: pairs of HIP events recorded around each fused-kernel launch on the
@@ -497,7 +499,31 @@ size_t chunk_begin(size_t n_blocks, int k, int K) {
 // carrier/NCO) at its offset, so each stage sees exactly the serial engine's inputs: the same
 // bits.  Events order chunk k's PLL after its band-pass and its audio after its PLL; the call
 // ends with the context stream waiting for the audio stream.
+int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm, float* d_mono,
+                              int K);
 int run_stereo_pipelined(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm, float* d_mono, int K) {
+    const int rc = run_stereo_pipelined_body(c, d_iq, n_blocks, d_pcm, d_mono, K);
+    if (rc != 0 && c->s_front) {
+        // a launch failed part-way: the context stream still waits for whatever the side streams
+        // hold, so a later call (or fmrx_synchronize) never races them
+        c->pll_trig.known = false;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (hipEventCreateWithFlags(&e0, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&e1, hipEventDisableTiming) == hipSuccess) {
+            (void)hipEventRecord(e0, c->s_front);
+            (void)hipEventRecord(e1, c->s_audio);
+            (void)hipStreamWaitEvent(c->stream, e0, 0);
+            (void)hipStreamWaitEvent(c->stream, e1, 0);
+            (void)hipStreamSynchronize(c->stream);
+        }
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+    }
+    return rc;
+}
+
+int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm, float* d_mono,
+                              int K) {
     const int ns = c->cfg.n_streams;
     const size_t ipb = c->geo.if_samples, n_if = n_blocks * ipb;
     for (int k = 0; k < K; k++)
@@ -512,7 +538,7 @@ int run_stereo_pipelined(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int1
         HIPCHK(hipStreamCreateWithPriority(&c->s_front, hipStreamNonBlocking, lo));
         HIPCHK(hipStreamCreateWithPriority(&c->s_audio, hipStreamNonBlocking, lo));
     }
-    const size_t n_ev = 2 * (size_t)K + 3;
+    const size_t n_ev = 3 * (size_t)K + 3;
     while (c->pipe_ev.size() < n_ev) {
         hipEvent_t e;
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -521,6 +547,7 @@ int run_stereo_pipelined(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int1
     hipEvent_t ev_start = c->pipe_ev[0], ev_end = c->pipe_ev[1], ev_lane = c->pipe_ev[2 * (size_t)K + 2];
     auto ev_bp = [&](int k) { return c->pipe_ev[2 + 2 * (size_t)k]; };
     auto ev_pll = [&](int k) { return c->pipe_ev[3 + 2 * (size_t)k]; };
+    auto ev_nco = [&](int k) { return c->pipe_ev[2 * (size_t)K + 3 + (size_t)k]; };
     // both side streams start after everything enqueued on the context stream so far
     HIPCHK(hipEventRecord(ev_start, c->stream));
     HIPCHK(hipStreamWaitEvent(c->s_front, ev_start, 0));
@@ -529,6 +556,7 @@ int run_stereo_pipelined(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int1
     for (int k = 0; k < K; k++)
         max_m = std::max(max_m, (chunk_begin(n_blocks, k + 1, K) - chunk_begin(n_blocks, k, K)) * ipb);
     if ((rc = c->d_pll_side.ensure(pll_side_doubles((int)max_m, ns)))) return rc;
+    if ((rc = c->d_pll_side2.ensure(pll_side_doubles((int)max_m, ns)))) return rc;
     AudioLaunch A{};
     A.demod = c->d_demod.p;
     A.demod_stride = c->demod_stride;
@@ -552,10 +580,14 @@ int run_stereo_pipelined(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int1
     size_t lane_m = 0;
     if (c->pll_trig.known && c->pll_trig.lo == c->pll_trig.hi && c->pll_trig.lo < (double)kPllIdxMin)
         lane_m = (size_t)((double)kPllIdxMin - c->pll_trig.lo);
-    auto pll = [&](size_t off, size_t m) -> int {
+    // a chunk's PLL leaves its NCO (filter.cpp:170, a parallel pass) to the audio stream, so the
+    // context stream goes on to the next chunk's runners; chunk k's trigArgs stay in side buffer
+    // k & 1 until that NCO has read them (the context stream waits for it before chunk k + 2)
+    auto side_of = [&](int k) { return (k & 1) ? c->d_pll_side2.p : c->d_pll_side.p; };
+    auto pll = [&](size_t off, size_t m, double* side, bool nco) -> int {
         if (m == 0) return 0;
         if (launch_pll(c->d_carrier.p + off, (int)m, ns, n_if, 19000.0f, (float)c->geo.if_fs, 2.0f, 0.0f, 0.01f,
-                       c->d_pll.p, c->d_pll_side.p, c->stream, c->hint(c->pll_trig), c->pll_stats)) {
+                       c->d_pll.p, side, c->stream, c->hint(c->pll_trig), c->pll_stats, nco)) {
             c->pll_trig.known = false;
             return fail(FMRX_EHIP, "PLL launch failed");
         }
@@ -588,13 +620,20 @@ int run_stereo_pipelined(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int1
         HIPCHK(hipEventRecord(ev_bp(k), c->s_front));
         // the context stream: the PLL of chunk k (project.cpp:166)
         HIPCHK(hipStreamWaitEvent(c->stream, ev_bp(k), 0));
+        if (k >= 2) HIPCHK(hipStreamWaitEvent(c->stream, ev_nco(k - 2), 0));  // side buffer k & 1 read
         const size_t m0 = k == 0 ? std::min(lane_m, m) : 0;
-        if ((rc = pll(off, m0))) return rc;
+        if ((rc = pll(off, m0, side_of(k), true))) return rc;  // (the lane part: its NCO in place)
         if (k == 0 && lane_m > 0) HIPCHK(hipEventRecord(ev_lane, c->stream));
-        if ((rc = pll(off + m0, m - m0))) return rc;
+        if ((rc = pll(off + m0, m - m0, side_of(k), false))) return rc;
         HIPCHK(hipEventRecord(ev_pll(k), c->stream));
-        // s_audio: the audio stage of chunk k (and the state carry after the last)
+        // s_audio: the NCO and the audio stage of chunk k (and the state carry after the last)
         HIPCHK(hipStreamWaitEvent(c->s_audio, ev_pll(k), 0));
+        const int t_nco = c->stage_timer.begin(c->s_audio);
+        if (launch_pll_nco(c->d_carrier.p + off + m0, (int)(m - m0), ns, n_if, 2.0f, 0.0f, c->d_pll.p, side_of(k),
+                           c->s_audio))
+            return fail(FMRX_EHIP, "NCO launch failed");
+        c->stage_timer.end(t_nco, kStNco, 0.0, c->s_audio);
+        HIPCHK(hipEventRecord(ev_nco(k), c->s_audio));
         const int t_au = c->stage_timer.begin(c->s_audio);
         if (launch_stereo_audio_range(A, (int)b0, (int)b1, last, ns, c->s_audio))
             return fail(FMRX_EHIP, "stereo audio launch failed");
@@ -786,7 +825,7 @@ void fmrx_destroy(fmrx_ctx* c) {
     c->d_audio_hist.release(); c->d_demod.release(); c->d_channel.release(); c->d_carrier.release();
     c->d_pll.release(); c->d_mix_tail.release(); c->d_mono_state.release(); c->d_in.release();
     c->d_out.release(); c->d_f32.release(); c->d_scratch.release(); c->d_sintab.release();
-    c->d_pll_side.release();
+    c->d_pll_side.release(); c->d_pll_side2.release();
     c->d_rds_taps.release(); c->d_rds_dhist.release(); c->d_rds_chan.release(); c->d_rds_car.release();
     c->d_rds_pll.release();
     for (auto& e : c->evs) {

@@ -104,9 +104,13 @@ struct PllHint {
     double trig_lo = 0.0, trig_hi = 0.0;
     StageTimer* timer = nullptr;  // diagnostic stage timing (null: off)
 };
+// nco = false: the NCO pass is left to the caller (launch_pll_nco with the same io, n, stride,
+// side and st, on any stream ordered after this launch and before `side` is reused).
 int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
                float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s,
-               const PllHint& hint, unsigned long long* spec_stats = nullptr);
+               const PllHint& hint, unsigned long long* spec_stats = nullptr, bool nco = true);
+int launch_pll_nco(float* io, int n, int n_streams, size_t stride, float nco_scale, float phase_adjust, float* st,
+                   const double* side, hipStream_t s);
 
 // pll_sat.hip: the saturated-segment runner over a launch_pll segment (pll_spec_lane_kernel's grid
 // and arguments; it runs the streams that one leaves to it)

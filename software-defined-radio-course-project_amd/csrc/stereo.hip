@@ -916,7 +916,7 @@ size_t pll_side_doubles(int n, int n_streams) {
 // certified pll_kernel in place.
 int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float fs,
                float nco_scale, float phase_adjust, float norm_bw, float* st, double* side, hipStream_t s,
-               const PllHint& hint, unsigned long long* spec_stats) {
+               const PllHint& hint, unsigned long long* spec_stats, bool nco) {
     if (n <= 0) return 0;
     const size_t seg = pll_seg_len(n, n_streams);
     const size_t rb = seg / kPllBatch;
@@ -1096,10 +1096,25 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         j = e;
     }
     // the NCO of every sample from its trigArg (filter.cpp:170), in parallel, over the input in place
-    timed(kStNco, 0.0, [&] {
-        hipLaunchKernelGGL(pll_nco_kernel, dim3((n + 255) / 256, n_streams), dim3(256), 0, s, io, n, stride,
-                           spec ? args : io, spec ? (size_t)n : stride, nco_scale, phase_adjust, st);
-    });
+    if (nco)
+        timed(kStNco, 0.0, [&] {
+            hipLaunchKernelGGL(pll_nco_kernel, dim3((n + 255) / 256, n_streams), dim3(256), 0, s, io, n, stride,
+                               spec ? args : io, spec ? (size_t)n : stride, nco_scale, phase_adjust, st);
+        });
+    else if (!spec)  // the trigArgs are in io itself: launch_pll_nco reads them from `side`
+        (void)hipMemcpy2DAsync(reinterpret_cast<float*>(side + 4 * seg * (size_t)n_streams), (size_t)n * sizeof(float),
+                               io, stride * sizeof(float), (size_t)n * sizeof(float), n_streams,
+                               hipMemcpyDeviceToDevice, s);
+    return ok();
+}
+
+int launch_pll_nco(float* io, int n, int n_streams, size_t stride, float nco_scale, float phase_adjust, float* st,
+                   const double* side, hipStream_t s) {
+    if (n <= 0) return 0;
+    const size_t seg = pll_seg_len(n, n_streams);
+    const float* args = reinterpret_cast<const float*>(side + 4 * seg * (size_t)n_streams);  // n per stream
+    hipLaunchKernelGGL(pll_nco_kernel, dim3((n + 255) / 256, n_streams), dim3(256), 0, s, io, n, stride, args,
+                       (size_t)n, nco_scale, phase_adjust, st);
     return ok();
 }
 
