@@ -488,7 +488,7 @@ def test_stereo_pipelined_chunks(fmrx, orc, monkeypatch, mode, n_streams, nb, ch
     front end + band-pass of chunk k + 1 and audio of chunk k - 1 on their own HIP streams beside
     the PLL of chunk k, every chunk reading the call's buffers at its offset (a chunk's RF halo
     is the call's own bytes in front of it).  FMRX_STEREO_CHUNKS forces the chunk count (None: the
-    default, 8 from 64 streams, fewer when a chunk would hold < 2^14 samples); two calls in a row
+    default, 8 from 16 streams, fewer when a chunk would hold < 2^14 samples); two calls in a row
     check the carried state.  Modes 0/1 take the tiled audio kernel, mode 2 the per-frame one."""
     if chunks is not None:
         monkeypatch.setenv("FMRX_STEREO_CHUNKS", chunks)
