@@ -48,6 +48,7 @@ namespace fmrx {
 // barrier wait, summed over every batch and workgroup, printed at exit
 __device__ unsigned long long g_pred_prof[6];
 __device__ unsigned long long g_pipe_prof[6];
+__device__ unsigned long long g_pipe_prof_w2[2];  // wave 2's body / barrier wait
 __device__ unsigned long long g_idx_prof[6];
 // redos per stream (blockIdx.x) and form: pipe 16-step, pipe 64-step five, pipe three, index
 constexpr int kProfStreams = 4096;
@@ -811,13 +812,24 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                         check(i - 1);
                         const int redo = __builtin_amdgcn_readfirstlane(smiss[(i - 2) & 3]);
                         if (redo) {
-                            __syncthreads();  // the chain redoes intervals i - 2 .. i
-                            __syncthreads();
-                            if (i + 1 <= ni) {  // interval i + 1 again, from the corrected phase
+                            // the chain redoes interval i - 2 exactly, then runs i - 1 again on
+                            // its candidates (from the phase at i - 2's start, which was right)
+                            // and i on candidates predicted anew here from the corrected phase
+                            __syncthreads();  // B1: the chain's exact redo of i - 2 follows
+                            __syncthreads();  // B1.5: i - 2's exact end state is in the ring
+                            {
+                                float v;
+                                ld(i, v);
+                                put(i, sst[(i - 2) & 3][BPI - 1].y, v);
+                            }
+                            __syncthreads();  // B2: the chain ran i - 1 again
+                            check(i - 1);
+                            if (i + 1 <= ni) {  // interval i + 1 from the phase at i's start
                                 float v;
                                 ld(i + 1, v);
                                 put(i + 1, sst[(i - 1) & 3][BPI - 1].y, v);
                             }
+                            __syncthreads();  // B3: the chain ran i again
                         }
                         const unsigned long long p1 = PROF_T();
                         __syncthreads();
@@ -833,6 +845,10 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         if (t == 0 && w == 1) {
             atomicAdd(&g_pipe_prof[2], ev_body);
             atomicAdd(&g_pipe_prof[3], ev_wait);
+        }
+        if (t == 0 && w == 2) {
+            atomicAdd(&g_pipe_prof_w2[0], ev_body);
+            atomicAdd(&g_pipe_prof_w2[1], ev_wait);
         }
 #endif
         (void)ev_body;
@@ -869,10 +885,9 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
     __syncthreads();  // (prologue)
     unsigned long long ch_body = 0, ch_wait = 0, n_redo = 0, n_inj = 0;
-    for (int i = 1; i <= ni; i++) {
-        const unsigned long long p0 = PROF_T();
+    // interval i on the fast chain from (integ, phase) and the carry, its data in ring slot i & 3
+    auto run = [&](int i) {
         const int is = i & 3;
-        const int flag = smiss[(i - 2) & 3];  // the verdict on interval i - 2 (slot 3 is clear at i = 1)
         // in bursts of CH steps: the data, 1.25 CH (NC = 5: 2.25 CH) 16-byte reads at once in the
         // order the steps need them (spread over the steps they stall the chain more,
         // tools/ubench_chain.hip), then the steps, then the batch states
@@ -941,32 +956,40 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             },
             std::make_integer_sequence<int, NI / CH>{});
         sexact[is] = 0;
+    };
+    for (int i = 1; i <= ni; i++) {
+        const unsigned long long p0 = PROF_T();
+        const int flag = smiss[(i - 2) & 3];  // the verdict on interval i - 2 (slot 3 is clear at i = 1)
+        run(i);
         if (__builtin_amdgcn_readfirstlane(flag)) {
             n_redo++;
-            // the inject hook's interval counts once it is redone, whichever verdict started the
-            // redo (a real miss on the interval before it clears the hook's own verdict)
-            n_inj += (inj >= i - 2 && inj <= i) ? 1 : 0;
-            __syncthreads();  // E2's stores of interval i - 1 happen before the redo's
-            // intervals i - 2 (missed), i - 1 and i exactly, from the state at the start of i - 2
-            // (the end of interval i - 3 in the ring; interval 0 is batch 0, slot 0 holds its end)
+            n_inj += inj == i - 2 ? 1 : 0;  // the inject hook's interval, redone exactly
+            __syncthreads();  // B1: E2's stores of interval i - 1 happen before the redo's
+            // interval i - 2 (missed) exactly, from the state at its start (the end of interval
+            // i - 3 in the ring; interval 0 is batch 0, slot 0 holds its end)
             const int f = i - 2;
             const float2 r0 = sst[(f - 1) & 3][BPI - 1];
             const float a = (float)(pr_at(j0(f) - 1) + (double)r0.y);  // the trigArg before it
             PllState q;
             PllCtx c{};
             pll_state_at(q, c, r0.x, r0.y, trig0, (long long)j0(f), a, DeviceLib{});
-            for (int k = f; k <= i; k++) {
-                exact(q, c, j0(k), j0(k) + NI);
-                if (t == 0) {
-                    sst[k & 3][BPI - 1] = make_float2(q.integ, q.phase);
-                    if (k > f) sexact[k & 3] = 1;
-                }
+            exact(q, c, j0(f), j0(f) + NI);
+            if (t == 0) {
+                sst[f & 3][BPI - 1] = make_float2(q.integ, q.phase);
+                sexact[f & 3] = 1;
+                smiss[(i - 1) & 3] = 0;  // E2's verdict on the wrong interval i - 1
             }
-            if (t == 0) smiss[(i - 1) & 3] = 0;  // E2's verdict on the wrong interval i - 1
             integ = q.integ;
             phase = q.phase;
-            carry_exact((float)c.x, i + 1);
-            __syncthreads();  // the evaluators redo interval i + 1 from here
+            carry_exact((float)c.x, f + 1);
+            __syncthreads();  // B1.5: the evaluators predict interval i anew from i - 2's end
+            // interval i - 1 again on the fast chain: its candidates came from the phase at the
+            // start of i - 2, which was right; E2 checks it again after B2
+            run(i - 1);
+            __syncthreads();  // B2: interval i's new candidates are in; E2 checks i - 1, the
+                              // evaluators predict i + 1 from i - 1's end
+            run(i);
+            __syncthreads();  // B3
         }
         const unsigned long long p1 = PROF_T();
         __syncthreads();
@@ -1327,6 +1350,11 @@ static void print_pred_prof() {
                              tot, n, mx, arg);
         }
     }
+    unsigned long long h2[2] = {};
+    (void)hipMemcpyFromSymbol(h2, HIP_SYMBOL(g_pipe_prof_w2), sizeof h2);
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pipe_prof), sizeof h) == hipSuccess && h[4])
+        std::fprintf(stderr, "pll_pipe prof: wave 2 body %.1f wait %.1f (shader cycles per interval)\n",
+                     (double)h2[0] / h[4], (double)h2[1] / h[4]);
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pipe_prof), sizeof h) == hipSuccess && h[4])
         std::fprintf(stderr, "pll_pipe prof: intervals %llu chain body %.1f wait %.1f, evaluator body %.1f wait %.1f "
                      "(shader cycles per interval), %llu redos\n", h[4], (double)h[0] / h[4], (double)h[1] / h[4],
