@@ -49,6 +49,7 @@ namespace fmrx {
 __device__ unsigned long long g_pred_prof[6];
 __device__ unsigned long long g_pipe_prof[6];
 __device__ unsigned long long g_pipe_prof_w2[2];  // wave 2's body / barrier wait
+__device__ unsigned long long g_miss_reason[3];   // pll_pipe_kernel's missed steps by reason
 __device__ unsigned long long g_idx_prof[6];
 // redos per stream (blockIdx.x) and form: pipe 16-step, pipe 64-step five, pipe three, index
 constexpr int kProfStreams = 4096;
@@ -713,6 +714,13 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                                 (NC == 3 || (tt.z > -__builtin_inff() && tt.w > -__builtin_inff()));
             const uint32_t idx = __builtin_bit_cast(uint32_t, a) - cm;
             const bool cert = idx < (uint32_t)NC && scert[sl][J][idx < (uint32_t)NC ? idx : 0] != 0;
+#ifdef FMRX_AB_PROF
+            // why a step misses: its trigArg outside the candidates / its e uncertified / a threshold
+            // outside its window
+            if (idx >= (uint32_t)NC) atomicAdd(&g_miss_reason[0], 1ull);
+            else if (!cert) atomicAdd(&g_miss_reason[1], 1ull);
+            if (!thr_ok) atomicAdd(&g_miss_reason[2], 1ull);
+#endif
             return !cert || !thr_ok || !(c0 > 0.0f && c0 < 3.0e38f);
         };
         auto check = [&](int k) {
@@ -1350,6 +1358,10 @@ static void print_pred_prof() {
                              tot, n, mx, arg);
         }
     }
+    unsigned long long mr[3] = {};
+    if (hipMemcpyFromSymbol(mr, HIP_SYMBOL(g_miss_reason), sizeof mr) == hipSuccess && (mr[0] | mr[1] | mr[2]))
+        std::fprintf(stderr, "pll_pipe missed steps: trigArg outside the candidates %llu, e uncertified %llu, "
+                     "threshold outside its window %llu\n", mr[0], mr[1], mr[2]);
     unsigned long long h2[2] = {};
     (void)hipMemcpyFromSymbol(h2, HIP_SYMBOL(g_pipe_prof_w2), sizeof h2);
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pipe_prof), sizeof h) == hipSuccess && h[4])

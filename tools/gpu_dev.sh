@@ -46,6 +46,7 @@ for step in "$@"; do
     predict) timeout -k 10 300 python tools/make_carrier.py /tmp/carrier.f32 72 > $OUT/predict.txt 2>&1 || { tail $OUT/predict.txt; exit 11; }
              g++ -O2 -ffp-contract=off -o /tmp/pll_predict tools/pll_predict.cpp || exit 11
              timeout -k 10 600 /tmp/pll_predict /tmp/carrier.f32 2 >> $OUT/predict.txt 2>&1 || { tail $OUT/predict.txt; exit 11; }
+             grep -A20 "extrapolated centre" $OUT/predict.txt | head -24
              tail -40 $OUT/predict.txt ;;
     ktrace) timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/kt_c4 -o run --output-format csv -- \
               python3 tools/stage_times.py --no-gib --single 0 > $OUT/kt_c4.log 2>&1 || { tail $OUT/kt_c4.log; exit 14; }

@@ -49,7 +49,7 @@ int main(int argc, char** argv) {
     const float Kp = nb * (float)2.666, Ki = nb * nb * (float)3.555;
     const double w = 2 * 3.14159265358979323846 * (double)(19000.0f / 240000.0f);
     const size_t N = x.size();  // steps from 2^24 on: trigOffset stuck (pll_sat.hip's regime)
-    std::vector<float> phase(N), arg(N);
+    std::vector<float> phase(N), arg(N), integs(N);
     float integ = 0, ph = 0, fbI = 1, fbQ = 0, trig = 0;
     for (size_t i = 0; i < N; i++) {
         const float eI = x[i] * fbI, eQ = x[i] * (-fbQ);
@@ -59,6 +59,7 @@ int main(int argc, char** argv) {
         trig = trig + 1.0f;
         const float a = (float)(w * (double)trig + (double)ph);
         phase[i] = ph;
+        integs[i] = integ;
         arg[i] = a;
         fbI = (float)std::cos((double)a);
         fbQ = (float)std::sin((double)a);
@@ -134,6 +135,40 @@ int main(int argc, char** argv) {
             std::printf("[2^%-4.1f, 2^%-4.1f)     %5d  step hit %.4f  batch hit %.4f\n", std::log2((double)j0),
                         std::log2((double)j1), B, (double)hit / (double)(j1 - j0), (double)nb_ok / nb_all);
         }
+    }
+    // the candidates centred on an extrapolated phase: phase_ref + integ_ref (j - s) (the phase
+    // moves by about integ a step, filter.cpp:161-162), s the step of the reference state; the
+    // fraction of B-step batches whose every step is within m floats of that centre
+    std::printf("B-step batches within m floats of the extrapolated centre, lookback %d:\n", lb);
+    std::printf("%-22s %s\n", "j range", "m = 0 1 2 3 4");
+    for (int B : {16, 64})
+    for (int e = 17; e < 25; e++) {
+        const size_t j0 = (size_t)1 << e, j1 = std::min(e == 24 ? N : ((size_t)1 << (e + 1)), N);
+        if (j0 >= j1) continue;
+        long nb_all = 0, ok[5] = {}, okc[5] = {};
+        for (size_t b0 = j0; b0 + B <= j1; b0 += B) {
+            const size_t back = (size_t)(lb - 1) * B + 1;
+            const size_t sref = b0 - back;
+            const float p0 = phase[sref], i0 = integs[sref];
+            long kmax = 0, kmaxc = 0;
+            for (size_t j = b0; j < b0 + B; j++) {
+                const double pr = w * (double)std::min((float)(j + 1), 16777216.0f);
+                const float cand = (float)(pr + (double)p0 + (double)i0 * (double)(j - sref));
+                kmax = std::max(kmax, std::labs(ulps_between(cand, arg[j])));
+                const float cand0 = (float)(pr + (double)p0);
+                kmaxc = std::max(kmaxc, std::labs(ulps_between(cand0, arg[j])));
+            }
+            nb_all++;
+            for (int q = 0; q < 5; q++) {
+                ok[q] += kmax <= q;
+                okc[q] += kmaxc <= q;
+            }
+        }
+        std::printf("[2^%d, 2^%d)  B=%-3d extrap", e, e + 1, B);
+        for (int q = 0; q < 5; q++) std::printf(" %.5f", (double)ok[q] / nb_all);
+        std::printf("   plain");
+        for (int q = 0; q < 5; q++) std::printf(" %.5f", (double)okc[q] / nb_all);
+        std::printf("\n");
     }
     // below 2^22: fraction of B-step batches whose every step is within m floats of c0 (2m + 1
     // candidates), per octave of j -- how many candidates a chain would need there
