@@ -617,11 +617,6 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     // branch and loop after it stay scalar
     auto uni = [](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v))); };
     PllState p{uni(S[0]), uni(S[1]), uni(S[2]), uni(S[3]), uni(S[5])};
-#ifdef FMRX_AB_EXCL
-    // A/B: every wave of the runner claims its SIMD's whole register file (a clobber of the last
-    // AGPR), so no wave of another kernel can share a SIMD with the serial chain or its evaluators
-    asm volatile("" ::: "a255");
-#endif
     // the variant's domain (uniform over the group): NC = 3 from 2^22; NC = 5 with 64-step
     // intervals in [2^21, 2^22), with 16-step ones in [2^20, 2^21)
     const bool in_domain = NC == 3 ? pll_pipe_stream(p.trig, step, kPllPipeMin)
@@ -1101,11 +1096,6 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
     const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
     auto uni = [](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v))); };
     PllState p{uni(S[0]), uni(S[1]), uni(S[2]), uni(S[3]), uni(S[5])};
-#ifdef FMRX_AB_EXCL
-    // A/B: every wave of the runner claims its SIMD's whole register file (a clobber of the last
-    // AGPR), so no wave of another kernel can share a SIMD with the serial chain or its evaluators
-    asm volatile("" ::: "a255");
-#endif
     const bool in_domain = pll_pipe_stream(p.trig, step, lo, hi);
     const float trig0 = p.trig;
     const double t0d = (double)trig0;
