@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/gpu_dev.sh <tag> [steps...] — development GPU call: each named step under its own time
 # limit, stopping at the first failure.  Steps: tests (whole GPU suite), pll (PLL / stereo tests
-# only), n2 (the N=2 bench line rehearsed with gloo, both ranks on device 0), mfma (tools/ubench_mfma_add), predict (tools/pll_predict.cpp on a 72 s GPU-made carrier, lookback 2), rprof22 (runner_prof of the 64-step forms from 2^21, 2^22, 2^23 with the profiling build), rprof (tools/runner_prof.py per form, with the FMRX_AB_PROF build), testsall (whole GPU suite, not stopping at a failure), idx (the index-runner tests), ubench (tools/ubench_idx), stages (tools/stage_times.py), stages1 (configs[4] with the serial engine), pipe (the pipelined-engine tests), s32 (configs[4]-length calls at 32 streams, serial vs 8 chunks), libab (stage_times per A/B build in $LIBS, alternating, twice), redoc4 (configs[4] with the FMRX_AB_PROF build: runner cycles and redos per stream), ktrace (kernel trace of configs[4] calls + tools/trace_overlap.py), bench (bench.py, no CPU baseline), smoke.
+# only), n2 (the N=2 bench line rehearsed with gloo, both ranks on device 0), mfma (tools/ubench_mfma_add), predict (tools/pll_predict.cpp on a 72 s GPU-made carrier, lookback 2), rprof22 (runner_prof of the 64-step forms from 2^21, 2^22, 2^23 with the profiling build), rprof (tools/runner_prof.py per form, with the FMRX_AB_PROF build), testsall (whole GPU suite, not stopping at a failure), idx (the index-runner tests), ubench (tools/ubench_idx), stages (tools/stage_times.py), stages1 (configs[4] with the serial engine), pipe (the pipelined-engine tests), s32 (configs[4]-length calls at 32 streams, serial vs 8 chunks), envab (configs[4] per value of $ENVVAR in $VALS, alternating, twice), libab (stage_times per A/B build in $LIBS, alternating, twice), redoc4 (configs[4] with the FMRX_AB_PROF build: runner cycles and redos per stream), ktrace (kernel trace of configs[4] calls + tools/trace_overlap.py), bench (bench.py, no CPU baseline), smoke.
 set -o pipefail
 TAG=${1:-dev}; shift
 OUT=gpurun_out/$TAG
@@ -72,6 +72,12 @@ for step in "$@"; do
                python tools/runner_prof.py --load /tmp/rp_states.npz --trig $tr >> $OUT/runner_prof22.txt 2>&1 || { tail $OUT/runner_prof22.txt; exit 10; }
            done
            grep -v amdgpu.ids $OUT/runner_prof22.txt ;;
+    envab) # configs[4] calls with each value of $ENVVAR in $VALS, alternating, twice
+            for r in 1 2; do for v in $VALS; do
+              env $ENVVAR=$v timeout -k 10 300 python tools/stage_times.py --no-gib --single 0 \
+                > $OUT/envab_${r}_$v.json 2>> $OUT/envab.err || { tail $OUT/envab.err; exit 18; }
+              echo "$r $ENVVAR=$v $(python -c "import json,sys; j=json.load(open(sys.argv[1])); print({k: v['wall_s'] for k, v in j.items()}, {k: round(x['ms'],1) for k, x in j['configs[4]']['stages'].items() if 'runner' in k})" $OUT/envab_${r}_$v.json)"
+            done; done ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail $OUT/smoke.log; exit 5; }
            tail -1 $OUT/smoke.log ;;
   esac
