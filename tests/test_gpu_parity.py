@@ -504,6 +504,25 @@ def test_stereo_pipelined_chunks(fmrx, orc, monkeypatch, mode, n_streams, nb, ch
         assert np.array_equal(np.concatenate([a[s], b[s]]), want), s
 
 
+def test_stereo_pipelined_checkpoint_resume(fmrx, orc, monkeypatch):
+    """The pipelined engine's carried state (demod history, PLL with its trigOffset hint, mixer
+    tail, mono delay; api.cpp run_stereo_pipelined) through a checkpoint: 16 streams (the
+    engine's default threshold) in pipelined calls, the blob into a second context, which goes
+    on pipelined, bit-exact against the oracle on three streams."""
+    monkeypatch.setenv("FMRX_STEREO_CHUNKS", "3")
+    ns, nb, bb = 16, 30, 12800
+    iq = np.stack([iqgen.make(f"synth:{620 + k}", 2 * nb * bb) for k in range(ns)])
+    with fmrx.Receiver(0, fmrx.STEREO, n_streams=ns) as rx:
+        a = rx.process(np.ascontiguousarray(iq[:, :nb * bb]))
+        blob = rx.get_state()
+    with fmrx.Receiver(0, fmrx.STEREO, n_streams=ns) as rx2:
+        rx2.set_state(blob)
+        b = rx2.process(np.ascontiguousarray(iq[:, nb * bb:]))
+    for s in (0, 7, 15):
+        want = orc.run(0, 51, iq[s], ["pcm"])["pcm"]
+        assert np.array_equal(np.concatenate([a[s], b[s]]), want), s
+
+
 @pytest.mark.parametrize("channels,n_streams", [(2, 70), (1, 130), (2, 1100), (2, 4200)])
 def test_many_streams_cross_wave_boundaries(fmrx, orc, channels, n_streams):
     """Many streams of different content: the PLL runs one stream per wave until the streams
