@@ -1,14 +1,14 @@
 #!/usr/bin/env python3
 """End-to-end drop-in timing: stdin u8 I/Q -> stdout S16, the `fmrx` CLI
-(pipelined: pinned ring of 3 batch slots, H2D / receive / D2H overlapped) beside the
-reference's own `project` executable (oracle/_ref/project, built from src/*.cpp in place).
+(pipelined: pinned ring of 3 batch slots, H2D / receive / D2H overlapped).
 
     python tools/bench_cli.py [--mib 1024] [--mode 0] [--batch 2048]
 
-Writes the synthetic stream to a file first (untimed), then times each program reading it on
-stdin and writing a file.  The reference exits at EOF with blocks still queued
-(project.cpp:51-54), so its stereo PCM is checked as a bit-exact PREFIX of fmrx's.  Prints
-one JSON line.
+Writes the synthetic stream to a file first (untimed), then times each CLI form reading it on
+stdin and writing a file.  Prints one JSON line.  The reference's own `project` on the same
+1 GiB stream is timed by bench.py's cpu_baseline leg (configs[2] "threaded_project"), the only
+place a measurement runs anything under oracle/; its stereo bytes are compared with the CLI's
+in tests/test_gpu_parity.py (test_cli_*).
 """
 import argparse
 import json
@@ -22,7 +22,6 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tests"))
-sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 
 def main():
@@ -30,14 +29,13 @@ def main():
     ap.add_argument("--mib", type=int, default=1024)
     ap.add_argument("--mode", type=int, default=0)
     ap.add_argument("--batch", type=int, default=2048)
-    ap.add_argument("--no-reference", action="store_true")
     args = ap.parse_args()
 
     import iqgen
-    import oracle
 
     fm = iqgen.load_fmrx()
-    bb, rf_fs = oracle.MODES[args.mode][0], oracle.MODES[args.mode][3]
+    geo = fm.geometry(fm.default_config(args.mode, fm.STEREO))
+    bb, rf_fs = geo.block_bytes, geo.rf_fs
     nbytes = args.mib << 20
     tmp = tempfile.mkdtemp(prefix="fmrx_cli_", dir="/tmp")
     src = os.path.join(tmp, "iq.u8")
@@ -54,25 +52,17 @@ def main():
     runs = [("fmrx_stereo", [exe, str(args.mode), "2", "--batch", str(args.batch)]),
             ("fmrx_channels1", [exe, str(args.mode), "1", "--batch", str(args.batch)]),
             ("fmrx_mono_product", [exe, str(args.mode), "1", "--mono-product", "--batch", str(args.batch)])]
-    ref = os.path.join(REPO, "oracle", "_ref", "project")
-    if not args.no_reference and os.path.exists(ref):
-        runs.append(("reference_project", [ref, str(args.mode), "2"]))
     for name, cmd in runs:
         dst = os.path.join(tmp, name + ".s16")
         with open(src, "rb") as fi, open(dst, "wb") as fo:
             t0 = time.perf_counter()
             r = subprocess.run(cmd, stdin=fi, stdout=fo, stderr=subprocess.PIPE, timeout=900)
             dt = time.perf_counter() - t0
-        # the reference ends with exit(1) at EOF by design (project.cpp:51-54)
-        if r.returncode != 0 and name != "reference_project":
+        if r.returncode != 0:
             raise SystemExit(f"{name} failed: {r.stderr.decode()[-500:]}")
         outs[name] = np.fromfile(dst, np.int16)
         res[name] = {"seconds": round(dt, 3), "MS_per_s": round(nbytes / 2 / dt / 1e6, 2),
                      "x_realtime": round(nbytes / 2 / rf_fs / dt, 1), "pcm_bytes": int(outs[name].nbytes)}
-    if "reference_project" in outs:
-        a, b = outs["reference_project"], outs["fmrx_stereo"]
-        res["reference_prefix_bit_exact"] = bool(len(a) <= len(b) and np.array_equal(a, b[: len(a)]))
-        res["reference_blocks_written"] = int(len(a) // (2 * oracle.MODES[args.mode][2]))
     res["channels1_equals_stereo"] = bool(np.array_equal(outs["fmrx_channels1"], outs["fmrx_stereo"]))
     for f in os.listdir(tmp):
         os.remove(os.path.join(tmp, f))

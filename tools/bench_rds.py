@@ -18,7 +18,6 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tests"))
-sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 
 def main():
@@ -30,10 +29,10 @@ def main():
     import torch
 
     import iqgen
-    import oracle
 
     fm = iqgen.load_fmrx()
-    nif, bp_fs = oracle.MODES[args.mode][1], oracle.MODES[args.mode][5]
+    geo = fm.geometry(fm.default_config(args.mode, fm.STEREO))
+    nif, bp_fs = geo.if_samples, geo.bp_fs
     nb = int(args.seconds * bp_fs) // nif
     base = iqgen.make_rds_demod(3, nb * nif, bp_fs)
     for ns in (int(v) for v in args.streams.split(",")):
