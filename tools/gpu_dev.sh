@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/gpu_dev.sh <tag> [steps...] — development GPU call: each named step under its own time
 # limit, stopping at the first failure.  Steps: tests (whole GPU suite), pll (PLL / stereo tests
-# only), n2 (the N=2 bench line rehearsed with gloo, both ranks on device 0), mfma (tools/ubench_mfma_add), predict (tools/pll_predict.cpp on a 72 s GPU-made carrier, lookback 2), rprof22 (runner_prof of the 64-step forms from 2^21, 2^22, 2^23 with the profiling build), rprof (tools/runner_prof.py per form, with the FMRX_AB_PROF build), testsall (whole GPU suite, not stopping at a failure), idx (the index-runner tests), ubench (tools/ubench_idx), stages (tools/stage_times.py), stages1 (configs[4] with the serial engine), pipe (the pipelined-engine tests), s32 (configs[4]-length calls at 32 streams, serial vs 8 chunks), envab (configs[4] per value of $ENVVAR in $VALS, alternating, twice), libab (stage_times per A/B build in $LIBS, alternating, twice), redoc4 (configs[4] with the FMRX_AB_PROF build: runner cycles and redos per stream), ktrace (kernel trace of configs[4] calls + tools/trace_overlap.py), bench (bench.py, no CPU baseline), smoke.
+# only), n2 (the N=2 bench line rehearsed with gloo, both ranks on device 0), mfma (tools/ubench_mfma_add), predict (tools/pll_predict.cpp on a 72 s GPU-made carrier, lookback 2), rprof22 (runner_prof of the forms at $TRIGS, default the 64-step forms from 2^21, 2^22, 2^23, with the profiling build), rprof (tools/runner_prof.py per form, with the FMRX_AB_PROF build), testsall (whole GPU suite, not stopping at a failure), idx (the index-runner tests), ubench (tools/ubench_idx), stages (tools/stage_times.py), stages1 (configs[4] with the serial engine), pipe (the pipelined-engine tests), s32 (configs[4]-length calls at 32 streams, serial vs 8 chunks), envab (configs[4] per value of $ENVVAR in $VALS, alternating, twice), libab (stage_times per A/B build in $LIBS, alternating, twice), redoc4 (configs[4] with the FMRX_AB_PROF build: runner cycles and redos per stream), ktrace (kernel trace of configs[4] calls + tools/trace_overlap.py), bench (bench.py, no CPU baseline), smoke.
 set -o pipefail
 TAG=${1:-dev}; shift
 OUT=gpurun_out/$TAG
@@ -65,9 +65,10 @@ for step in "$@"; do
     s32) for k in 1 8; do FMRX_STEREO_CHUNKS=$k timeout -k 10 300 python tools/stage_times.py --streams 32 --no-gib --single 0 \
             > $OUT/stages32_k$k.json 2>> $OUT/s32.err || { tail $OUT/s32.err; exit 17; }
           echo "k=$k $(python -c "import json,sys; j=json.load(open(sys.argv[1])); print({k: v['wall_s'] for k, v in j.items()})" $OUT/stages32_k$k.json)"; done ;;
-    rprof22) timeout -k 10 120 python tools/runner_prof.py --save /tmp/rp_states.npz --trig 2097152 --trig 4194304 --trig 8388608 \
+    rprof22) TR=${TRIGS:-2097152 4194304 8388608}
+           timeout -k 10 120 python tools/runner_prof.py --save /tmp/rp_states.npz $(for t in $TR; do echo --trig $t; done) \
                > $OUT/runner_prof22.txt 2>&1 || { tail $OUT/runner_prof22.txt; exit 10; }
-           for tr in 2097152 4194304 8388608; do
+           for tr in $TR; do
              FMRX_LIB_PATH=software-defined-radio-course-project_amd/build_ab/libfmrx.so timeout -k 10 120 \
                python tools/runner_prof.py --load /tmp/rp_states.npz --trig $tr >> $OUT/runner_prof22.txt 2>&1 || { tail $OUT/runner_prof22.txt; exit 10; }
            done
