@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/gpu_dev.sh <tag> [steps...] — development GPU call: each named step under its own time
 # limit, stopping at the first failure.  Steps: tests (whole GPU suite), pll (PLL / stereo tests
-# only), n2 (the N=2 bench line rehearsed with gloo, both ranks on device 0), mfma (tools/ubench_mfma_add), predict (tools/pll_predict.cpp on a 72 s GPU-made carrier, lookback 2), rprof22 (runner_prof of the forms at $TRIGS, default the 64-step forms from 2^21, 2^22, 2^23, with the profiling build), rprof (tools/runner_prof.py per form, with the FMRX_AB_PROF build), testsall (whole GPU suite, not stopping at a failure), idx (the index-runner tests), ubench (tools/ubench_idx), stages (tools/stage_times.py), stages1 (configs[4] with the serial engine), pipe (the pipelined-engine tests), s32 (configs[4]-length calls at 32 streams, serial vs 8 chunks), envab (configs[4] per value of $ENVVAR in $VALS, alternating, twice), libab (stage_times per A/B build in $LIBS, alternating, twice), redoc4 (configs[4] with the FMRX_AB_PROF build: runner cycles and redos per stream), ktrace (kernel trace of configs[4] calls + tools/trace_overlap.py), bench (bench.py, no CPU baseline), smoke.
+# only), n2 (the N=2 bench line rehearsed with gloo, both ranks on device 0), mfma (tools/ubench_mfma_add), predict (tools/pll_predict.cpp on a 72 s GPU-made carrier, lookback 2), rprof22 (runner_prof of the forms at $TRIGS, default the 64-step forms from 2^21, 2^22, 2^23, with the profiling build), rprof (tools/runner_prof.py per form, with the FMRX_AB_PROF build), testsall (whole GPU suite, not stopping at a failure), idx (the index-runner tests), ubench (tools/ubench_idx), stages (tools/stage_times.py), stages1 (configs[4] with the serial engine), pipe (the pipelined-engine tests), s32 (configs[4]-length calls at 32 streams, serial vs 8 chunks), envab (configs[4] per value of $ENVVAR in $VALS, alternating, twice), libab (stage_times per A/B build in $LIBS, alternating, twice), redoc4 (configs[4] with the FMRX_AB_PROF build: runner cycles and redos per stream), ktrace (kernel trace of configs[4] calls + tools/trace_overlap.py), bench (bench.py, no CPU baseline), clitrace (rocprofv3 stats of `fmrx 0 2` over 1 GiB, per runner form), smoke.
 set -o pipefail
 TAG=${1:-dev}; shift
 OUT=gpurun_out/$TAG
@@ -73,6 +73,13 @@ for step in "$@"; do
                python tools/runner_prof.py --load /tmp/rp_states.npz --trig $tr >> $OUT/runner_prof22.txt 2>&1 || { tail $OUT/runner_prof22.txt; exit 10; }
            done
            grep -v amdgpu.ids $OUT/runner_prof22.txt ;;
+    clitrace) # kernel stats of the CLI over 1 GiB of the bench stream (full kernel names: runner forms per range)
+            timeout -k 10 200 python -c "import sys; sys.path.insert(0, 'tests'); import iqgen; fm = iqgen.load_fmrx(); f = open('/tmp/iq1g.u8', 'wb'); [f.write(fm.synth_host(5, 2400000, p, 1 << 25).tobytes()) for p in range(0, 1 << 29, 1 << 25)]; f.close()" || exit 19
+            timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt_cli -o run --output-format csv -- \
+              software-defined-radio-course-project_amd/bin/fmrx 0 2 --batch 2048 < /tmp/iq1g.u8 > /tmp/cli.s16 2> $OUT/kt_cli.err || { tail $OUT/kt_cli.err; exit 19; }
+            f=$(ls $OUT/kt_cli/*/run_kernel_stats.csv $OUT/kt_cli/run_kernel_stats.csv 2>/dev/null | head -1)
+            python tools/kernel_stats_summary.py $f > $OUT/cli_kernel_classes.json && cat $OUT/cli_kernel_classes.json
+            ls -la /tmp/cli.s16 ;;
     envab) # configs[4] calls with each value of $ENVVAR in $VALS, alternating, twice
             for r in 1 2; do for v in $VALS; do
               env $ENVVAR=$v timeout -k 10 300 python tools/stage_times.py --no-gib --single 0 \
