@@ -1410,10 +1410,16 @@ void launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t
     if (n <= 0) return;
     static_assert(kPllIdxWaves == 4, "the chain and three evaluators");
     if (form == 17)
-        hipLaunchKernelGGL((pll_idx_kernel<64, 3>), dim3(n_streams), dim3(256), 0, s, io, n, n_streams, stride, step,
+#ifndef FMRX_IDX17_NC
+#define FMRX_IDX17_NC 64
+#endif
+        hipLaunchKernelGGL((pll_idx_kernel<FMRX_IDX17_NC, 3>), dim3(n_streams), dim3(256), 0, s, io, n, n_streams, stride, step,
                            norm_bw, st, out, ostride, inject, miss, 131072.0f, 262143.0f, stats);
     else if (form == 18)
-        hipLaunchKernelGGL((pll_idx_kernel<32, 3>), dim3(n_streams), dim3(256), 0, s, io, n, n_streams, stride, step,
+#ifndef FMRX_IDX18_NC
+#define FMRX_IDX18_NC 32
+#endif
+        hipLaunchKernelGGL((pll_idx_kernel<FMRX_IDX18_NC, 3>), dim3(n_streams), dim3(256), 0, s, io, n, n_streams, stride, step,
                            norm_bw, st, out, ostride, inject, miss, 262144.0f, 524287.0f, stats);
     else
         hipLaunchKernelGGL((pll_idx_kernel<16, 3>), dim3(n_streams), dim3(256), 0, s, io, n, n_streams, stride, step,

@@ -947,7 +947,10 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     // (FMRX_PLL_PRED=2, tests: the two-wave runner even where its waves share SIMDs)
     const int pred_ok = [] {
         const char* e = std::getenv("FMRX_PLL_PRED");
-        return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
+#ifndef FMRX_PLL_IDX_DEFAULT
+#define FMRX_PLL_IDX_DEFAULT 1  // (A/B builds: -DFMRX_PLL_IDX_DEFAULT=2)
+#endif
+        return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : (e && e[0] == '1') ? 1 : FMRX_PLL_IDX_DEFAULT;
     }();
     int spw = 1;
     while (spw < 64 && (long long)spw * n_simd < n_streams) spw *= 2;
@@ -993,7 +996,10 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     // (FMRX_PLL_IDX=2: also its 64-candidate form from 2^17)
     const int idx_env = [] {
         const char* e = std::getenv("FMRX_PLL_IDX");
-        return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
+#ifndef FMRX_PLL_IDX_DEFAULT
+#define FMRX_PLL_IDX_DEFAULT 1  // (A/B builds: -DFMRX_PLL_IDX_DEFAULT=2)
+#endif
+        return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : (e && e[0] == '1') ? 1 : FMRX_PLL_IDX_DEFAULT;
     }();
     const bool idx = pipe && idx_env && kPllIdxWaves * n_streams <= n_simd;
     const double fast_min = idx ? (double)(idx_env == 2 ? kPllIdxMin64 : kPllIdxMin) : (double)kPllPipeMinLow;
