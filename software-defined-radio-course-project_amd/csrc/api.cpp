@@ -574,9 +574,10 @@ int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks,
     A.down = c->geo.audio_down;
     A.at = c->geo.audio_taps_total;
     A.audio_c = c->d_audio.p;
-    // the PLL of chunk 0 in two launches when its streams start below the index runner's range:
-    // the lane runner's segments first (issue-bound: a front-end wave sharing its SIMD halves its
-    // rate), then the rest; chunk 1's front end waits for the first part
+    // the PLL of chunk 0 in two launches when its streams start below 2^18: the lane runner's
+    // segments and the index runner's [2^17, 2^18) form first (issue-bound: a front-end wave
+    // sharing a chain's SIMD halves its rate), then the rest; chunk 1's front end waits for the
+    // first part
     size_t lane_m = 0;
     if (c->pll_trig.known && c->pll_trig.lo == c->pll_trig.hi && c->pll_trig.lo < (double)kPllIdxMin)
         lane_m = (size_t)((double)kPllIdxMin - c->pll_trig.lo);

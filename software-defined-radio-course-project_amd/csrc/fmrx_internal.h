@@ -138,15 +138,16 @@ void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_
                      unsigned long long* stats);
 
 // pll_pred.hip: the index runner (one stream a workgroup of four waves, spw == 1) for trigOffset
-// in [2^17, 2^20), self-certifying like launch_pll_pipe, same arguments; form 17: 64 candidates
+// in [2^17, 2^20), self-certifying like launch_pll_pipe, same arguments; form 17: 32 candidates
 // ([2^17, 2^18)), 18: 32 ([2^18, 2^19)), 19: 16 ([2^19, 2^20)).  A stream outside the form's
 // domain runs the range exactly.
 void launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
                     float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats);
 constexpr int kPllIdxWaves = 4;  // waves a stream: the chain and three evaluators, one SIMD each
-// the index runner's lowest trigOffset: 2^18.  Its 64-candidate form for [2^17, 2^18) is slower
-// than the lane runner there (113 vs 75 ns a step: 1,024 candidate evaluations an interval on its
-// three evaluator waves, profiles/r04/val/stages.json), so it runs only with FMRX_PLL_IDX=2
+// the index runner's lowest trigOffset: 2^17 (kPllIdxMin64; 2^18, kPllIdxMin, with FMRX_PLL_IDX=1).  In
+// [2^17, 2^18) 32 candidates (c0 - 16 .. c0 + 15) run 62 ns a step with their misses redone,
+// against the lane runner's 75; 64 took 113 (1,024 candidate evaluations an interval on three
+// evaluator waves, profiles/r04/val/stages.json; profiles/r04/ab_idx17_nc32/)
 constexpr float kPllIdxMin = 262144.0f;
 constexpr float kPllIdxMin64 = 131072.0f;
 

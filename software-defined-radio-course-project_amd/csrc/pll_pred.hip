@@ -1047,8 +1047,9 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
 // intervals between a prediction and its use, so three or five candidates miss; 16 to 64 do not
 // (tools/pll_predict.cpp, profiles/r04/pll_predict_below_2_20.txt: 16-step intervals from the
 // phase one interval back hit with 64 candidates on 0.9999+ of them in [2^17, 2^18), with 32 in
-// [2^18, 2^19), with 16 in [2^19, 2^20)).  Compares against NC - 1 thresholds would cost the
-// chain 2 (NC - 1) instructions a step, so here the chain forms the step's trigArg itself --
+// [2^18, 2^19), with 16 in [2^19, 2^20); the [2^17, 2^18) form runs 32 (~0.99 of intervals hit,
+// the misses redone: faster than 64 evaluations a step, profiles/r04/ab_idx17_nc32/)).  Compares
+// against NC - 1 thresholds would cost the chain 2 (NC - 1) instructions a step, so here the chain forms the step's trigArg itself --
 // float(P + (double)phase), filter.cpp:165, three instructions -- and turns it into a lane index:
 // the NC candidates of a step c0 - NC/2 .. c0 + NC/2 - 1 sit in NC consecutive lanes of one VGPR
 // row (64 / NC steps a row), so e = v_readlane(row, bits(trigArg) - base) with
@@ -1411,7 +1412,7 @@ void launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t
     static_assert(kPllIdxWaves == 4, "the chain and three evaluators");
     if (form == 17)
 #ifndef FMRX_IDX17_NC
-#define FMRX_IDX17_NC 64
+#define FMRX_IDX17_NC 32
 #endif
         hipLaunchKernelGGL((pll_idx_kernel<FMRX_IDX17_NC, 3>), dim3(n_streams), dim3(256), 0, s, io, n, n_streams, stride, step,
                            norm_bw, st, out, ostride, inject, miss, 131072.0f, 262143.0f, stats);

@@ -947,10 +947,7 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     // (FMRX_PLL_PRED=2, tests: the two-wave runner even where its waves share SIMDs)
     const int pred_ok = [] {
         const char* e = std::getenv("FMRX_PLL_PRED");
-#ifndef FMRX_PLL_IDX_DEFAULT
-#define FMRX_PLL_IDX_DEFAULT 1  // (A/B builds: -DFMRX_PLL_IDX_DEFAULT=2)
-#endif
-        return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : (e && e[0] == '1') ? 1 : FMRX_PLL_IDX_DEFAULT;
+        return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
     }();
     int spw = 1;
     while (spw < 64 && (long long)spw * n_simd < n_streams) spw *= 2;
@@ -992,14 +989,11 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     // the three-wave runner: every stream at the same known trigOffset t, a SIMD per wave (one
     // stream a workgroup of three); it takes the samples from trigOffset 2^20 on
     const bool pipe = spec && pred_ok && pipe_env && spw == 1 && 3 * n_streams <= n_simd && k && hlo == hhi;
-    // the index runner in [2^18, 2^20) wants four SIMDs a stream (FMRX_PLL_IDX=0: not launched)
-    // (FMRX_PLL_IDX=2: also its 64-candidate form from 2^17)
+    // the index runner in [2^17, 2^20) wants four SIMDs a stream (FMRX_PLL_IDX=0: not launched;
+    // FMRX_PLL_IDX=1: from 2^18 only, the lane runner keeping [2^17, 2^18))
     const int idx_env = [] {
         const char* e = std::getenv("FMRX_PLL_IDX");
-#ifndef FMRX_PLL_IDX_DEFAULT
-#define FMRX_PLL_IDX_DEFAULT 1  // (A/B builds: -DFMRX_PLL_IDX_DEFAULT=2)
-#endif
-        return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : (e && e[0] == '1') ? 1 : FMRX_PLL_IDX_DEFAULT;
+        return (e && e[0] == '0') ? 0 : (e && e[0] == '1') ? 1 : 2;
     }();
     const bool idx = pipe && idx_env && kPllIdxWaves * n_streams <= n_simd;
     const double fast_min = idx ? (double)(idx_env == 2 ? kPllIdxMin64 : kPllIdxMin) : (double)kPllPipeMinLow;

@@ -869,17 +869,21 @@ def test_pll_pipe_redo(fmrx, orc, monkeypatch, trig0, miss):
 
 @pytest.mark.parametrize("trig0", [131072.0, 262177.0, 524188.0, 600000.0, 1043576.0, 125000.0])
 @pytest.mark.parametrize("inject", [None, "5"])
-@pytest.mark.parametrize("idx", ["1", "0", "2"])
+@pytest.mark.parametrize("idx", ["1", "0", "2", None])
 def test_pll_index_runner(fmrx, orc, monkeypatch, trig0, inject, idx):
-    """trigOffset in [2^18, 2^20): the index runner (pll_pred.hip pll_idx_kernel: the chain forms
-    trigArg itself and reads its e from a lane of a candidate row -- 32 candidates from 2^18, 16
-    from 2^19; with FMRX_PLL_IDX=2 also 64 from 2^17), starting at 2^17 (the lane runner hands
-    over at 2^18), at 2^18 + 33, 100 steps below 2^19 (the 2^18 form hands over to the 2^19 one
+    """trigOffset in [2^17, 2^20): the index runner (pll_pred.hip pll_idx_kernel: the chain forms
+    trigArg itself and reads its e from a lane of a candidate row -- 32 candidates from 2^17 and
+    from 2^18, 16 from 2^19; FMRX_PLL_IDX=1: from 2^18 only, the lane runner below), starting at
+    2^17 (the default, FMRX_PLL_IDX=2 or unset, starts there; with 1 the lane runner hands over at
+    2^18), at 2^18 + 33, 100 steps below 2^19 (the 2^18 form hands over to the 2^19 one
     inside the call), at 600,000, and 5,000 steps below 2^20 (the three-wave runner takes over);
     125,000 starts on the lane runner and crosses into it.  FMRX_PLL_IDX=0: the lane runner below
     2^20.  Bit-exact against the oracle; a forced miss
     (FMRX_PLL_SPEC_INJECT) is redone exactly, and without it no batch is."""
-    monkeypatch.setenv("FMRX_PLL_IDX", idx)
+    if idx is None:
+        monkeypatch.delenv("FMRX_PLL_IDX", raising=False)
+    else:
+        monkeypatch.setenv("FMRX_PLL_IDX", idx)
     if inject is not None:
         monkeypatch.setenv("FMRX_PLL_SPEC_INJECT", inject)
     n = 20000
@@ -936,13 +940,14 @@ def test_pll_index_redo(fmrx, orc, monkeypatch, trig0, miss):
 def test_index_runner_streams(fmrx, monkeypatch):
     """pll_idx_kernel over many streams (200: four waves each still fit the SIMDs), every stream
     put at trigOffset 2^18 - 4,000 through the state blob (the runners need the streams at one
-    known trigOffset: the 2^17 form hands over to the 2^18 one inside the call), 24 blocks in one
-    call: the PCM equals the same call with the index runner off (FMRX_PLL_IDX=0: the lane
-    runner, checked by pll_check_kernel), and no batch is redone."""
+    known trigOffset: the 2^17 form hands over to the 2^18 one inside the call; FMRX_PLL_IDX=1:
+    the lane runner to 2^18), 24 blocks in one call: the PCM equals the same call with the index
+    runner off (FMRX_PLL_IDX=0: the lane runner, checked by pll_check_kernel), and no batch is
+    redone."""
     ns, nb, bb = 200, 24, 12800
     ins = np.stack([iqgen.make("synth:%d" % (700 + s % 5), (nb + 2) * bb) for s in range(ns)])
     outs = []
-    for idx in ("1", "0"):
+    for idx in ("2", "1", "0"):
         monkeypatch.setenv("FMRX_PLL_IDX", idx)
         with fmrx.Receiver(0, fmrx.STEREO, n_streams=ns) as rx:
             rx.process(ins[:, : 2 * bb])
@@ -959,7 +964,7 @@ def test_index_runner_streams(fmrx, monkeypatch):
             rx.debug_pll_stats(None)
         resumed, checked = counts.cpu().tolist()
         assert checked > 0 and resumed == 0, (idx, resumed, checked)
-    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[0], outs[2]) and np.array_equal(outs[1], outs[2])
 
 
 def test_pipe_runner_streams(fmrx, monkeypatch):
