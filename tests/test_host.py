@@ -119,3 +119,20 @@ def test_build_flags_forbid_fma_and_fast_math():
     flags = " ".join(flags)
     assert "-ffp-contract=off" in flags and "-fno-fast-math" in flags
     assert "-ffast-math" not in flags.replace("-fno-fast-math", "")
+
+
+def test_product_and_tools_do_not_use_oracle():
+    """Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may touch oracle/:
+    the package (host bindings, HIP sources, CLI) and the measurement tools under tools/ neither
+    import it nor name a path under it."""
+    import glob
+    import re
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(root, "software-defined-radio-course-project_amd")
+    files = (glob.glob(os.path.join(pkg, "*.py")) + glob.glob(os.path.join(pkg, "csrc", "*")) +
+             glob.glob(os.path.join(pkg, "Makefile")) + glob.glob(os.path.join(root, "tools", "*.py")) +
+             glob.glob(os.path.join(root, "tools", "*.sh")) + glob.glob(os.path.join(root, "tools", "*.cpp")))
+    pat = re.compile(r"import oracle|from oracle|[\"']oracle[\"']|oracle/_ref|_ref/project")
+    bad = [f for f in files if os.path.isfile(f) and pat.search(open(f, errors="replace").read())]
+    assert files and not bad, bad
