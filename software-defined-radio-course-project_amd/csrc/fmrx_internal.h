@@ -137,13 +137,13 @@ void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_
                      float* st, float* out, size_t ostride, int inject, int miss, int form,
                      unsigned long long* stats);
 
-// pll_pred.hip: the index runner (one stream a workgroup of four waves, spw == 1) for trigOffset
+// pll_pred.hip: the index runner (one stream a workgroup of five waves, four for form 19; spw == 1) for trigOffset
 // in [2^17, 2^20), self-certifying like launch_pll_pipe, same arguments; form 17: 32 candidates
 // ([2^17, 2^18)), 18: 32 ([2^18, 2^19)), 19: 16 ([2^19, 2^20)).  A stream outside the form's
 // domain runs the range exactly.
 void launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
                     float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats);
-constexpr int kPllIdxWaves = 4;  // waves a stream: the chain and three evaluators, one SIMD each
+constexpr int kPllIdxWaves = 4;  // SIMDs a stream (a CU): the chain and three or four evaluator waves
 // the index runner's lowest trigOffset: 2^17 (kPllIdxMin64; 2^18, kPllIdxMin, with FMRX_PLL_IDX=1).  In
 // [2^17, 2^18) 32 candidates (c0 - 16 .. c0 + 15) run 62 ns a step with their misses redone,
 // against the lane runner's 75; 64 took 113 (1,024 candidate evaluations an interval on three

@@ -1409,18 +1409,22 @@ void launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t
     reg_pred_prof();
 #endif
     if (n <= 0) return;
-    static_assert(kPllIdxWaves == 4, "the chain and three evaluators");
+    static_assert(kPllIdxWaves == 4, "a CU a stream: the chain and the evaluators on its four SIMDs");
     if (form == 17)
 #ifndef FMRX_IDX17_NC
 #define FMRX_IDX17_NC 32
 #endif
-        hipLaunchKernelGGL((pll_idx_kernel<FMRX_IDX17_NC, 3>), dim3(n_streams), dim3(256), 0, s, io, n, n_streams, stride, step,
+#ifndef FMRX_IDX_NW
+#define FMRX_IDX_NW 4  // evaluator waves of the 32-candidate forms: two rows of candidates each
+                       // (three waves: three rows, evaluator-bound; profiles/r04/ab_idx_nw4/)
+#endif
+        hipLaunchKernelGGL((pll_idx_kernel<FMRX_IDX17_NC, FMRX_IDX_NW>), dim3(n_streams), dim3(64 * (1 + FMRX_IDX_NW)), 0, s, io, n, n_streams, stride, step,
                            norm_bw, st, out, ostride, inject, miss, 131072.0f, 262143.0f, stats);
     else if (form == 18)
 #ifndef FMRX_IDX18_NC
 #define FMRX_IDX18_NC 32
 #endif
-        hipLaunchKernelGGL((pll_idx_kernel<FMRX_IDX18_NC, 3>), dim3(n_streams), dim3(256), 0, s, io, n, n_streams, stride, step,
+        hipLaunchKernelGGL((pll_idx_kernel<FMRX_IDX18_NC, FMRX_IDX_NW>), dim3(n_streams), dim3(64 * (1 + FMRX_IDX_NW)), 0, s, io, n, n_streams, stride, step,
                            norm_bw, st, out, ostride, inject, miss, 262144.0f, 524287.0f, stats);
     else
         hipLaunchKernelGGL((pll_idx_kernel<16, 3>), dim3(n_streams), dim3(256), 0, s, io, n, n_streams, stride, step,
