@@ -137,10 +137,13 @@ int fmrx_fm_demod(fmrx_ctx* ctx, float* d_out, float* d_prev, const float* d_i,
                   const float* d_q, int n);
 /* d_io: PLL input, overwritten by the NCO output.  d_st: 6 floats {integrator, phaseEst,
  * feedbackI, feedbackQ, ncoOut_state, trigOffset} (in/out).  Every PLL (this call, stereo,
- * RDS) runs speculatively -- the serial loop without certification, every 16-sample batch
- * re-verified exactly in parallel, the certified path from the first batch that differs --
- * with the same bits either way; environment FMRX_PLL_SPEC=0 selects the plain certified
- * launch.                                                                                  */
+ * RDS) runs speculatively with the same bits as the certified recurrence: below trigOffset
+ * 2^17 (and without a known trigOffset) the serial loop runs uncertified and every 16-sample
+ * batch is re-verified exactly in parallel, the certified path resuming from the first batch
+ * that differs; from 2^17 the self-certifying runners (index, three-wave) prove each step as
+ * they go and redo a missed interval exactly themselves.  Knob FMRX_KNOB_PLL_SPEC 0 selects the
+ * plain certified launch.  fmrx_pll reads d_st's trigOffset back (4 bytes, a host
+ * synchronisation on the context stream) to choose the runners.                             */
 int fmrx_pll(fmrx_ctx* ctx, float* d_io, int n, float freq, float fs, float nco_scale,
              float phase_adjust, float norm_bw, float* d_st);
 int fmrx_mixer(fmrx_ctx* ctx, float* d_out, const float* d_a, const float* d_b, int n);
@@ -215,15 +218,45 @@ int fmrx_debug_mono_stamps(fmrx_ctx* ctx, unsigned long long* d_stamps, size_t n
  * d_counts[1].  Results are unchanged.  d_counts = NULL turns it off.                          */
 int fmrx_debug_pll_stats(fmrx_ctx* ctx, unsigned long long* d_counts);
 
+/* ---- diagnostic: per-stream redos of the self-certifying PLL runners ----------------------- */
+/* With d_counts set (n_streams x 4 u32 on the device, zeroed and owned by the caller), the stereo *
+ * calls add, per stream s, the intervals each self-certifying runner redid on the exact path      *
+ * (a trigArg outside its candidates or an uncertified step) to d_counts[4 s + f]: f = 0 index     *
+ * runner ([2^17, 2^20)), 1 three-wave 16-step form, 2 its 64-step five-candidate form, 3 the      *
+ * three-candidate form.  Results are unchanged.  d_counts = NULL turns it off.                     */
+int fmrx_debug_pll_redos(fmrx_ctx* ctx, unsigned* d_counts);
+
 /* ---- diagnostic: per-stage device time of the stereo engine ------------------------------ */
 /* op 1 arms (and clears) HIP event pairs around every stage launch of the following stereo     *
  * calls (ms of overlapping stages add up); op 0 reads, op -1 reads and disarms.  Stage k of     *
  * n_kinds: 0 RF front end, 1 band-pass pair, 2 PLL pre-pass, 3 lane runner, 4 two-wave          *
  * predicted runner, 5 saturated runner, 6/7/8 three-wave runner forms from trigOffset 2^20 /   *
- * 2^21 / 2^22, 9 check, 10 resume/tail, 11 NCO, 12 audio.  ms[k] = summed device time,          *
+ * 2^21 / 2^22, 9 check, 10 resume/tail, 11 NCO, 12 audio, 13/14/15 index runner forms from     *
+ * trigOffset 2^17 / 2^18 / 2^19.  ms[k] = summed device time,                                   *
  * launches[k] = launches, steps[k] = serial PLL steps a runner kind ran as its segment's only  *
  * runner (per stream chain; for ns per step of each regime).  Results are unchanged.           */
 int fmrx_debug_stage_timing(fmrx_ctx* ctx, int op, double* ms, double* steps, long* launches, int n_kinds);
+
+/* ---- diagnostic / test knobs of one context ----------------------------------------------- */
+/* None of them changes the output.  The tuning knobs pick which kernel form runs (A/B
+ * measurements); a new context takes them from the environment variable named beside each
+ * (read once, at fmrx_create).  The PLL test hooks make the runners do extra work that their
+ * exact paths then redo (bit-identical output, counted by fmrx_debug_pll_stats); they are set
+ * only here, never from the environment.  value: the knob's integer (the skew: samples).       */
+#define FMRX_KNOB_PLL_SPEC 0          /* 1 speculative runners, 0 the certified launch  FMRX_PLL_SPEC */
+#define FMRX_KNOB_PLL_SAT 1           /* 0: no saturated-segment runner                 FMRX_PLL_SAT  */
+#define FMRX_KNOB_PLL_PRED 2          /* 0 no predicted runners, 2 forced on            FMRX_PLL_PRED */
+#define FMRX_KNOB_PLL_PIPE 3          /* 0: no three-wave runner                        FMRX_PLL_PIPE */
+#define FMRX_KNOB_PLL_IDX 4           /* 2 index runner from 2^17, 1 from 2^18, 0 off  FMRX_PLL_IDX  */
+#define FMRX_KNOB_STEREO_CHUNKS 5     /* 0 auto, k chunks (1 the serial engine)   FMRX_STEREO_CHUNKS */
+#define FMRX_KNOB_MONO_SPLIT 6        /* -1 default, 0 equal, n/1024 older wave's    FMRX_MONO_SPLIT */
+#define FMRX_KNOB_BPF_TILE 7          /* 0: the per-output band-pass kernel             FMRX_BPF_TILE */
+#define FMRX_KNOB_HALO_KERNEL 8       /* 1: the separate halo kernel                 FMRX_HALO_KERNEL */
+#define FMRX_KNOB_PLL_INJECT 9        /* test hook: runners corrupt batch 1+(k+s)%(nb-1) of stream s  */
+#define FMRX_KNOB_PLL_PIPE_MISS 10    /* test hook: self-certifying runners miss interval k            */
+#define FMRX_KNOB_PLL_HINT_SKEW 11    /* test hook: host trigOffset bounds shifted by value samples    */
+#define FMRX_KNOB_PLL_CNT 12          /* bit f-17: count runner for form f's range        FMRX_PLL_CNT  */
+int fmrx_debug_set_knob(fmrx_ctx* ctx, int knob, double value);
 
 #ifdef __cplusplus
 }

@@ -122,12 +122,22 @@ struct fmrx_ctx {
     bool timing = false;
     unsigned long long* stamps = nullptr;  // fmrx_debug_mono_stamps (diagnostic)
     unsigned long long* pll_stats = nullptr;  // fmrx_debug_pll_stats (diagnostic)
+    unsigned* pll_redos = nullptr;            // fmrx_debug_pll_redos (diagnostic)
     StageTimer stage_timer;                   // fmrx_debug_stage_timing (diagnostic)
     // the pipelined stereo engine (run_stereo_pipelined): front-end / band-pass stream, audio
     // stream and their events, created at the first pipelined call
     hipStream_t s_front = nullptr, s_audio = nullptr;
     std::vector<hipEvent_t> pipe_ev;
     int n_simd = 1024;                        // SIMDs of cfg.device (4 per CU), set at creation
+    // switches (fmrx_debug_set_knob): the tuning ones from the environment once, at creation;
+    // none of them changes the output (the PLL test hooks make the runners redo work)
+    struct Knobs {
+        PllKnobs pll;
+        int stereo_chunks = 0;  // 0: by stream count and call length; k: k chunks (1: serial engine)
+        int mono_split = -1;    // -1: kOlderShare; 0: equal spans; n: the older wave's n / 1024
+        int bpf_tile = 1;       // 0: the per-output band-pass kernel
+        int halo_kernel = 0;    // 1: the separate halo_kernel after the fused one
+    } knobs;
     // bounds on the streams' trigOffset (PllHint) of the stereo and the RDS PLL: 0 after a reset,
     // advanced by every call's samples (the float increments stick at 2^24), re-read from the
     // blob by fmrx_set_state; unknown after a failed launch
@@ -142,6 +152,8 @@ struct fmrx_ctx {
     PllHint hint(const TrigTrack& t) const {
         PllHint h;
         h.n_simd = n_simd;
+        h.knobs = knobs.pll;
+        h.redos = pll_redos;
         h.known = t.known;
         h.trig_lo = t.lo;
         h.trig_hi = t.hi;
@@ -254,6 +266,7 @@ int run_rds(fmrx_ctx* c, const float* d_demod, size_t demod_stride, size_t n_if,
     L.bp_fs = (float)c->geo.bp_fs;
     L.n_if = (int)n_if;
     L.hint = c->hint(c->rds_trig);
+    L.hint.redos = nullptr;  // fmrx_debug_pll_redos counts the stereo PLL's streams only
     if (launch_rds(L, ns, c->stream)) {
         c->rds_trig.known = false;
         return fail(FMRX_EHIP, "RDS launch failed");
@@ -284,14 +297,13 @@ int mono_segments(const fmrx_ctx* c, long long n_if, int wg_per_cu = 0) {
 
 // Unequal shares for the two waves of a SIMD (mono_fused.hip mono_share): when the grid is
 // two resident waves per SIMD (segs even, >= 15/16 of 2 x the SIMD count, 8 workgroups per
-// CU), the first-dispatched wave takes kOlderShare/1024 of each span.  FMRX_MONO_SPLIT=<n>
-// overrides it (0 = equal segments; timing sweeps).  660 since round 3's latency cuts (sweeps of
+// CU), the first-dispatched wave takes kOlderShare/1024 of each span.  Knob mono_split = n
+// (FMRX_MONO_SPLIT at creation) overrides it (0 = equal segments; timing sweeps).  660 since round 3's latency cuts (sweeps of
 // 580-700 on two boxes, profiles/r03/split_sweep*/: 660 fastest on both, 1.2-1.6 % ahead of 620).
 constexpr int kOlderShare = 660;
 int mono_older_share(const fmrx_ctx* c, int segs) {
     const int n_simd = c->n_simd;
-    int share = kOlderShare;
-    if (const char* e = std::getenv("FMRX_MONO_SPLIT")) share = std::atoi(e);
+    const int share = c->knobs.mono_split < 0 ? kOlderShare : c->knobs.mono_split;
     if (share <= 0 || share >= 1024) return 0;
     const long long wgs = (long long)segs * c->cfg.n_streams;
     if ((segs & 1) != 0 || mono_wg_per_cu(c->geo.rf_decim) != 8 || wgs * 16 < 2LL * n_simd * 15 || wgs > 2LL * n_simd)
@@ -343,10 +355,9 @@ int run_fused(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm,
     L.audio = with_audio ? 1 : 0;
     // the halo update rides in the fused kernel when every stream row is 16-B aligned (halo
     // bytes and block bytes are multiples of 16); otherwise halo_kernel runs after it
-    const char* he = std::getenv("FMRX_HALO_KERNEL");  // =1: the separate halo_kernel (A/B timing)
     const bool fused_halo = (reinterpret_cast<uintptr_t>(L.iq) & 15) == 0 && L.stream_bytes % 16 == 0 &&
                             L.iq_stride % 16 == 0 && c->halo_bytes % 16 == 0 &&
-                            !(he && he[0] == '1');
+                            c->knobs.halo_kernel != 1;  // knob halo_kernel = 1: the separate kernel (A/B)
     L.halo_next = (last && fused_halo) ? c->d_halo[c->halo_cur ^ 1].p : nullptr;
     const int ad = c->geo.audio_up == 1 ? c->geo.audio_down : 5;
     std::pair<hipEvent_t, hipEvent_t>* ev = nullptr;
@@ -427,7 +438,7 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
     S.ca_c = c->ca.data();
     S.bp_taps = c->geo.bp_taps;
     const int t_bp = c->stage_timer.begin(c->stream);
-    if (launch_bpf_pair(S, ns, c->stream)) return fail(FMRX_EHIP, "band-pass launch failed");
+    if (launch_bpf_pair(S, ns, c->stream, c->knobs.bpf_tile != 0)) return fail(FMRX_EHIP, "band-pass launch failed");
     c->stage_timer.end(t_bp, kStBpf, 0.0, c->stream);
     // project.cpp:166: PLL(carrier, 19000, if_fs, 2, 0, 0.01, ...)
     if ((rc = c->d_pll_side.ensure(pll_side_doubles((int)n_if, ns)))) return rc;
@@ -468,11 +479,10 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
 // Chunks of the stereo pipeline for a call of n_blocks blocks a stream: the stage work beside
 // the serial PLL (front end, band-pass pair, NCO, audio) grows with the streams, the PLL's with
 // the samples a stream, so a call pipelines from 16 streams on when a chunk holds enough blocks.
-// FMRX_STEREO_CHUNKS=k forces k chunks (1: the serial engine).
+// Knob stereo_chunks = k (FMRX_STEREO_CHUNKS at creation) forces k chunks (1: the serial engine).
 int stereo_chunks(const fmrx_ctx* c, size_t n_blocks) {
     int k = c->cfg.n_streams >= 16 ? 8 : 1;  // 32 streams x 60 s: 0.423 vs 0.430 s (profiles/r04/g9)
-    const char* e = std::getenv("FMRX_STEREO_CHUNKS");
-    if (e) k = std::max(1, std::atoi(e));
+    if (c->knobs.stereo_chunks > 0) k = c->knobs.stereo_chunks;
     else
         while (k > 1 && n_blocks * c->geo.if_samples / (size_t)k < 16384) k--;  // >= 2^14 samples a chunk
     // a chunk past the first reads its RF halo from the call's own bytes in front of it: every
@@ -616,7 +626,7 @@ int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks,
         S.ca_c = c->ca.data();
         S.bp_taps = c->geo.bp_taps;
         const int t_bp = c->stage_timer.begin(c->s_front);
-        if (launch_bpf_pair(S, ns, c->s_front)) return fail(FMRX_EHIP, "band-pass launch failed");
+        if (launch_bpf_pair(S, ns, c->s_front, c->knobs.bpf_tile != 0)) return fail(FMRX_EHIP, "band-pass launch failed");
         c->stage_timer.end(t_bp, kStBpf, 0.0, c->s_front);
         HIPCHK(hipEventRecord(ev_bp(k), c->s_front));
         // the context stream: the PLL of chunk k (project.cpp:166)
@@ -726,6 +736,28 @@ int fmrx_geometry(const fmrx_config* cfg, fmrx_geometry_t* g) {
     return FMRX_OK;
 }
 
+// The tuning switches of a new context from the environment (A/B measurements: which runner or
+// kernel form runs, never what it computes).  The PLL test hooks are not read here: only
+// fmrx_debug_set_knob sets them, per context.
+static fmrx_ctx::Knobs knobs_from_env() {
+    fmrx_ctx::Knobs k;
+    auto get = [](const char* name, int def) {
+        const char* e = std::getenv(name);
+        return (e && *e) ? std::atoi(e) : def;
+    };
+    k.pll.spec = get("FMRX_PLL_SPEC", 1);
+    k.pll.sat = get("FMRX_PLL_SAT", 1);
+    k.pll.pred = get("FMRX_PLL_PRED", 1);
+    k.pll.pipe = get("FMRX_PLL_PIPE", 1);
+    k.pll.idx = get("FMRX_PLL_IDX", 2);
+    k.pll.cnt = get("FMRX_PLL_CNT", 0);
+    k.stereo_chunks = std::max(0, get("FMRX_STEREO_CHUNKS", 0));
+    k.mono_split = get("FMRX_MONO_SPLIT", -1);
+    k.bpf_tile = get("FMRX_BPF_TILE", 1);
+    k.halo_kernel = get("FMRX_HALO_KERNEL", 0);
+    return k;
+}
+
 int fmrx_create(const fmrx_config* cfg, fmrx_ctx** out) {
     if (!out) return fail(FMRX_EINVAL, "null output pointer");
     *out = nullptr;
@@ -756,6 +788,7 @@ int fmrx_create(const fmrx_config* cfg, fmrx_ctx** out) {
                     g.rf_decim);
     }
     if ((rc = set_device(c))) { delete c; return rc; }
+    c->knobs = knobs_from_env();
     {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess && cus > 0)
@@ -1261,6 +1294,7 @@ int fmrx_pll(fmrx_ctx* c, float* d_io, int n, float freq, float fs, float nco_sc
     HIPCHK(hipStreamSynchronize(c->stream));
     PllHint hint;
     hint.n_simd = c->n_simd;
+    hint.knobs = c->knobs.pll;
     hint.known = trig >= 0.0f && trig <= 16777216.0f && trig == std::floor(trig);
     hint.trig_lo = hint.trig_hi = hint.known ? (double)trig : 0.0;
     hint.timer = c->stage_timer.on ? &c->stage_timer : nullptr;
@@ -1407,6 +1441,38 @@ int fmrx_debug_stage_timing(fmrx_ctx* c, int op, double* ms, double* steps, long
         T.on = false;
         T.used = 0;
     }
+    return FMRX_OK;
+}
+
+int fmrx_debug_set_knob(fmrx_ctx* c, int knob, double value) {
+    CtxLock lock_(c);
+    if (!c) return fail(FMRX_EINVAL, "null context");
+    fmrx_ctx::Knobs& k = c->knobs;
+    const int v = (int)value;
+    switch (knob) {
+        case FMRX_KNOB_PLL_SPEC: k.pll.spec = v; break;
+        case FMRX_KNOB_PLL_SAT: k.pll.sat = v; break;
+        case FMRX_KNOB_PLL_PRED: k.pll.pred = v; break;
+        case FMRX_KNOB_PLL_PIPE: k.pll.pipe = v; break;
+        case FMRX_KNOB_PLL_IDX: k.pll.idx = v; break;
+        case FMRX_KNOB_STEREO_CHUNKS: k.stereo_chunks = std::max(0, v); break;
+        case FMRX_KNOB_MONO_SPLIT: k.mono_split = v; break;
+        case FMRX_KNOB_BPF_TILE: k.bpf_tile = v; break;
+        case FMRX_KNOB_HALO_KERNEL: k.halo_kernel = v; break;
+        case FMRX_KNOB_PLL_INJECT: k.pll.inject = v; break;
+        case FMRX_KNOB_PLL_PIPE_MISS: k.pll.pipe_miss = v; break;
+        case FMRX_KNOB_PLL_HINT_SKEW: k.pll.skew = value; break;
+        case FMRX_KNOB_PLL_CNT: k.pll.cnt = v; break;
+        default: return fail(FMRX_EINVAL, "unknown knob %d", knob);
+    }
+    return FMRX_OK;
+}
+
+// Diagnostic: per-stream redo counts of the self-certifying PLL runners (stereo calls).
+int fmrx_debug_pll_redos(fmrx_ctx* c, unsigned* d_counts) {
+    CtxLock lock_(c);
+    if (!c) return fail(FMRX_EINVAL, "null context");
+    c->pll_redos = d_counts;
     return FMRX_OK;
 }
 

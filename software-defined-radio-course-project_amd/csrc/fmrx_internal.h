@@ -42,7 +42,8 @@ struct StereoLaunch {
     const float* ca_c;
     int bp_taps;
 };
-int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s);
+// tiled = false: the per-output kernel (A/B measurements; same bits)
+int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s, bool tiled = true);
 // PLL over n samples of n_streams streams (state st, 8 floats per stream), then the NCO
 // (filter.cpp:136-174).  side: device scratch of pll_side_doubles(n, n_streams) doubles.
 // spec_stats (diagnostic, may be null): the speculative path adds the runner batches that did
@@ -98,8 +99,25 @@ struct StageTimer {
     }
 };
 
+// Per-context switches of the PLL launch (api.cpp fmrx_ctx::knobs; fmrx_debug_set_knob).  The
+// tuning ones pick which runners run (same bits either way) and are read from the environment
+// once, when the context is created; the test hooks make the runners do extra (redone) work --
+// the output stays the exact path's -- and are set only through fmrx_debug_set_knob.
+struct PllKnobs {
+    int spec = 1;        // 0: the plain certified launch (FMRX_PLL_SPEC)
+    int sat = 1;         // 0: no saturated-segment runner (FMRX_PLL_SAT)
+    int pred = 1;        // 0: no predicted runners; 2: the two-wave one even where waves share SIMDs
+    int pipe = 1;        // 0: no three-wave runner (FMRX_PLL_PIPE)
+    int idx = 2;         // index runner from 2^17 (2), from 2^18 (1), off (0) (FMRX_PLL_IDX)
+    int cnt = 0;         // bit f - 17: the count runner takes form f's range (FMRX_PLL_CNT)
+    int inject = -1;     // test hook: the runners corrupt batch 1 + (k + s) % (nb - 1) of stream s
+    int pipe_miss = -1;  // test hook: the self-certifying runners report interval k as missed
+    double skew = 0.0;   // test hook: the host's trigOffset bounds shifted by this many samples
+};
 struct PllHint {
     int n_simd = 1024;
+    PllKnobs knobs;
+    unsigned* redos = nullptr;  // fmrx_debug_pll_redos (diagnostic): n_streams x kPllRedoForms
     bool known = false;
     double trig_lo = 0.0, trig_hi = 0.0;
     StageTimer* timer = nullptr;  // diagnostic stage timing (null: off)
@@ -135,15 +153,29 @@ void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_str
 // runs.  stats (may be null): += batches redone exactly, batches run.
 void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
                      float* st, float* out, size_t ostride, int inject, int miss, int form,
-                     unsigned long long* stats);
+                     unsigned long long* stats, unsigned* redos = nullptr);
 
-// pll_pred.hip: the index runner (one stream a workgroup of five waves, four for form 19; spw == 1) for trigOffset
-// in [2^17, 2^20), self-certifying like launch_pll_pipe, same arguments; form 17: 32 candidates
-// ([2^17, 2^18)), 18: 32 ([2^18, 2^19)), 19: 16 ([2^19, 2^20)).  A stream outside the form's
-// domain runs the range exactly.
-void launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
-                    float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats);
-constexpr int kPllIdxWaves = 4;  // SIMDs a stream (a CU): the chain and three or four evaluator waves
+// pll_pred.hip: the index runner (one stream a workgroup: the chain and four evaluator waves
+// for forms 17 / 18, three for form 19 -- a CU a stream, two of the five waves sharing a SIMD),
+// self-certifying like launch_pll_pipe, same arguments; form 17: 32 candidates ([2^17, 2^18)),
+// 18: 32 ([2^18, 2^19)), 19: 16 ([2^19, 2^20)).  A stream outside the form's domain runs the
+// range exactly.  Returns non-zero when the form's workgroup cannot be resident on one CU (its
+// registers) or the launch fails.
+int launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
+                   float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats,
+                   unsigned* redos = nullptr);
+// pll_pred.hip: the count runner (pll_cnt_kernel: the chain picks each step's e by one compare of
+// the phase against a row of exact thresholds and a bit count), one stream a workgroup of five
+// waves (a CU), self-certifying, same arguments as launch_pll_idx; form 17 / 18: [2^17, 2^18) /
+// [2^18, 2^19), 31 candidates, 16-step intervals; 19: [2^19, 2^20), 15, 32 steps; 20: [2^20,
+// 2^21), 15, 64 steps; 21: [2^21, 2^22), 7, 64 steps.
+int launch_pll_cnt(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
+                   float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats,
+                   unsigned* redos = nullptr);
+// fmrx_debug_pll_redos: per stream, intervals the self-certifying runners redid, by form (0 index,
+// 1 three-wave 16-step, 2 three-wave 64-step five candidates, 3 three candidates)
+constexpr int kPllRedoForms = 4;
+constexpr int kPllIdxSimds = 4;  // SIMDs a stream takes: one CU (launch_pll admits n_simd / 4 streams)
 // the index runner's lowest trigOffset: 2^17 (kPllIdxMin64; 2^18, kPllIdxMin, with FMRX_PLL_IDX=1).  In
 // [2^17, 2^18) 32 candidates (c0 - 16 .. c0 + 15) run 62 ns a step with their misses redone,
 // against the lane runner's 75; 64 took 113 (1,024 candidate evaluations an interval on three

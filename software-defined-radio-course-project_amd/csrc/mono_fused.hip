@@ -627,13 +627,18 @@ long long mono_chunks(long long n_if, int /*rf_taps*/, int rf_decim, int /*audio
 
 int mono_wg_per_cu(int rf_decim) { return rf_decim == 9 ? 8 : kVariants[variant_index()].wg_per_cu; }
 
+#ifdef FMRX_AB_ABLATE
+// A/B build only (Makefile `ab`, AB=-DFMRX_AB_ABLATE; tools/gpu_ablate.sh): the stage-removal
+// bitmask from the environment -- timing experiments, results wrong by design, so never in the
+// product library
 int ablation() {
     static int a = [] {
-        const char* e = getenv("FMRX_ABLATE");  // timing experiments only (wrong results)
+        const char* e = getenv("FMRX_ABLATE");
         return e ? atoi(e) : 0;
     }();
     return a;
 }
+#endif
 
 template <int ABL>
 int launch_ablation(const MonoLaunch& L, int n_streams, const MonoTaps& taps, hipStream_t s) {
@@ -665,6 +670,7 @@ int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_de
     // clock / occupancy stamps (fmrx_debug_mono_stamps): the default kernel plus stamps
     if (L.stamps && rf_taps == 101 && rf_decim == 10 && audio_down == 5 && vi == kDefaultVariant)
         return launch_ablation<64>(L, n_streams, taps, s);
+#ifdef FMRX_AB_ABLATE
     if (const int a = ablation(); a != 0 && rf_taps == 101 && rf_decim == 10) {
         switch (a) {
             case 1: return launch_ablation<1>(L, n_streams, taps, s);
@@ -684,6 +690,7 @@ int launch_mono_fused(const MonoLaunch& L, int n_streams, int rf_taps, int rf_de
             default: break;
         }
     }
+#endif
     // the default variant skips tap 0 (Z0) when the designs have h[0] = +-0 (always, for the
     // context's own taps; both FIRs then), the sweep variants keep it
     const bool z0 = tap0_zero(taps.rf[0]) && (!L.audio || tap0_zero(taps.audio[0]));

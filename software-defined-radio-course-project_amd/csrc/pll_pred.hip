@@ -51,6 +51,7 @@ __device__ unsigned long long g_pipe_prof[6];
 __device__ unsigned long long g_pipe_prof_w2[2];  // wave 2's body / barrier wait
 __device__ unsigned long long g_miss_reason[3];   // pll_pipe_kernel's missed steps by reason
 __device__ unsigned long long g_idx_prof[6];
+__device__ unsigned long long g_cnt_prof[6];
 // redos per stream (blockIdx.x) and form: pipe 16-step, pipe 64-step five, pipe three, index
 constexpr int kProfStreams = 4096;
 __device__ unsigned int g_redo_stream[4][kProfStreams];
@@ -575,7 +576,7 @@ template <int NB, int BPI, int RD, int NC>
 __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))) pll_pipe_kernel(const float* io, int n, int n_streams, size_t stride,
                                                       double step, float norm_bw, float* st, float* out_base,
                                                       size_t ostride, int inject, int miss,
-                                                      unsigned long long* stats) {
+                                                      unsigned long long* stats, unsigned* redos) {
     constexpr int NI = NB * BPI;
     static_assert(NI == 16 || NI == 32 || NI == 64, "the evaluators' lane map: 64 / NI lanes a step");
     static_assert(NC == 3 || NC == 5, "three or five candidates");
@@ -1024,6 +1025,9 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             atomicAdd(stats, (n_inj + (unsigned long long)fin) * 3 * BPI);
             atomicAdd(stats + 1, (unsigned long long)nb);
         }
+        // fmrx_debug_pll_redos: this stream's redone intervals, by form (1: 16-step five
+        // candidates, 2: 64-step five, 3: three)
+        if (redos) atomicAdd(&redos[kPllRedoForms * (size_t)s + (NI == 16 ? 1 : NC == 5 ? 2 : 3)], (unsigned)n_redo);
     }
 #ifdef FMRX_AB_PROF
     if (t == 0) {
@@ -1072,7 +1076,8 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
 template <int NC, int NW>
 __global__ void __launch_bounds__(64 * (1 + NW)) __attribute__((amdgpu_waves_per_eu(1, 1)))
 pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step, float norm_bw, float* st,
-               float* out_base, size_t ostride, int inject, int miss, float lo, float hi, unsigned long long* stats) {
+               float* out_base, size_t ostride, int inject, int miss, float lo, float hi, unsigned long long* stats,
+               unsigned* redos) {
     constexpr int NI = 16;          // steps an interval
     constexpr int SPP = 64 / NC;    // steps a candidate row
     constexpr int NR = NI / SPP;    // candidate rows an interval
@@ -1320,8 +1325,324 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
             atomicAdd(stats, n_inj);  // "resumed": the inject hook's forced redos only
             atomicAdd(stats + 1, (unsigned long long)nb);
         }
+        if (redos) atomicAdd(&redos[kPllRedoForms * (size_t)s], (unsigned)n_redo);  // form 0: index
     }
-    (void)n_redo;
+}
+
+
+// ---- pll_cnt_kernel: one stream a workgroup of 1 + NW waves; the chain picks e by a count --------
+//
+// The exact phase threshold of every candidate (phase_thr_exact: "trigArg >= c" is "phase >=
+// T(c)", trigArg = float(P + (double)phase) being monotone in the float phase, filter.cpp:165)
+// turns the candidate choice into ONE compare of the phase against a row of thresholds: lane l of
+// step J's T row holds T(c_base + l) (l <= NC; +inf beyond), so the bits of the compare's mask
+// are a prefix and their count is the trigArg's place in the window, plus one.  Lane l of the E
+// row holds the e of candidate c_base + l - 1 (certified, NaN where not; lanes 0 and NC + 1 NaN:
+// a trigArg below or above the window), so e = v_readlane(E, count) -- a compare, s_bcnt1 and a
+// v_readlane whatever NC is (tools/ubench_cnt.hip mode 3: 60 cycles a step with the data in
+// registers, against 91 for the index runner's f64 trigArg and lane index, mode 0).  So the
+// window can be wide enough that a trigArg outside it is rare even for 64-step intervals
+// predicted 64 to 128 steps ahead (tools/pll_predict.cpp, profiles/r04/g5/predict.txt).
+//   the chain (wave 0), per step: e, (Ki e, Kp e), the three float updates (filter.cpp:161-162),
+//     the compare and count, the count recorded in lane J of a row.  After the interval: a NaN
+//     phase or carry e (a trigArg outside its window, an uncertified candidate) or a start state
+//     out of the certified range redoes the interval on the exact path at once, from the state at
+//     its start (the evaluators' next interval came from that state: no restart);
+//   the evaluators (waves 1 .. NW), per interval k: interval k + 1's T and E rows from the phase
+//     at interval k's start (c0 = float(P + phase_ref), c_base = c0 - NC / 2), items spread over
+//     all their lanes; wave 1 also stores interval k - 1's trigArgs (c_base + count - 1: the
+//     candidate IS the trigArg) unless the chain redid it.
+// Exact by construction as pll_pipe_kernel / pll_idx_kernel.
+
+// The smallest float phase f with float(P + (double)f) >= c (phase_thr's T), always found: when
+// phase_thr's window of four neighbours does not hold it (rare), a bisection over the ordered
+// float line (32 halvings; "reaches" is monotone in f).
+__device__ inline uint32_t fkey(float f) {
+    const uint32_t b = __builtin_bit_cast(uint32_t, f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ inline float fkey_inv(uint32_t k) {
+    return __builtin_bit_cast(float, (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+__device__ inline float phase_thr_exact(double P, uint32_t cb) {
+    const float T = phase_thr(P, cb);
+    if (T > -__builtin_inff()) return T;
+    const float c = __builtin_bit_cast(float, cb);
+    uint32_t lo = fkey(-__builtin_inff()), hi = fkey(__builtin_inff());  // reaches(lo) false, (hi) true
+    for (int it = 0; it < 34 && hi - lo > 1u; it++) {
+        const uint32_t mid = lo + (hi - lo) / 2u;
+        if (reaches(P, fkey_inv(mid), c)) hi = mid;
+        else lo = mid;
+    }
+    return fkey_inv(hi);
+}
+
+template <int NI, int NC, int NW>
+__global__ void __launch_bounds__(64 * (1 + NW)) __attribute__((amdgpu_waves_per_eu(1, 1)))
+pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step, float norm_bw, float* st,
+               float* out_base, size_t ostride, int inject, int miss, float lo, float hi, unsigned long long* stats,
+               unsigned* redos) {
+    constexpr int NP = NC + 2;  // row slots: T(c_base + l) l <= NC, +inf | NaN, e(c_base + l - 1), NaN
+    constexpr int HC = NC / 2;  // candidates c0 - HC .. c0 + HC
+    constexpr int RD = 4;       // intervals of step inputs in flight
+    constexpr int EV = 64 * NW;                    // evaluator lanes
+    constexpr int NE = (NI * NC + EV - 1) / EV;    // e items a lane an interval
+    constexpr int NT = (NI * (NC + 1) + EV - 1) / EV;  // threshold items a lane an interval
+    constexpr int CH = NI < 16 ? NI : 16;          // the chain's steps a burst of reads
+    static_assert(NC % 2 == 1 && NP <= 64, "an odd window within a wave");
+    static_assert(NI == 16 || NI == 32 || NI == 64, "a row of counts in a VGPR");
+    // rings of four intervals (interval k in slot k & 3): the T and E rows of each step, bits(c_base)
+    // - 1 of each step (the trigArg store), the chain's count of each step, its (integ, phase) at
+    // the interval's end, "redone exactly"
+    __shared__ float sT[4][NI][NP];
+    __shared__ float sE[4][NI][NP];
+    __shared__ uint32_t sbase[4][NI];
+    __shared__ int srow[4][NI];
+    __shared__ float2 sst[4];
+    __shared__ int sexact[4];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
+    const int s = blockIdx.x;  // grid = n_streams
+    const float* x = io + (size_t)s * stride;
+    float* out = out_base + (size_t)s * ostride;
+    float* S = st + 8 * (size_t)s;
+    const float Kp = norm_bw * static_cast<float>(2.666);
+    const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
+    auto uni = [](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v))); };
+    PllState p{uni(S[0]), uni(S[1]), uni(S[2]), uni(S[3]), uni(S[5])};
+    const bool in_domain = pll_pipe_stream(p.trig, step, lo, hi);
+    const float trig0 = p.trig;
+    const double t0d = (double)trig0;
+    auto pr_at = [&](long long j) {
+        return step * (double)(float)fmin(t0d + (double)(j + 1), (double)kPllTrigStick);
+    };
+    const int nb = n / NI;
+    const int ni = nb > 0 ? nb - 1 : 0;  // intervals after interval 0 (exact)
+    // test hook: a forced miss on interval 1 + (inject + s) % ni (counted as resumed)
+    const int inj = inject >= 0 && ni > 0 ? 1 + (inject + s) % ni : -1;
+    auto exact = [&](PllState& q, PllCtx& c, long long j0, long long j1) {
+        if (j1 > j0) {
+            const PllPair z = pll_redo(q, c, x + j0, out + j0, (int)(j1 - j0), Ki, Kp, step, true);
+            q = z.p;
+            c = z.ctx;
+        }
+    };
+    if (ni < 2 || !in_domain) {
+        if (w == 0) {
+            PllCtx c{};
+            c.valid = false;
+            exact(p, c, 0, n);
+            if (t == 0) {
+                S[0] = p.integ; S[1] = p.phase; S[2] = p.fbI; S[3] = p.fbQ; S[5] = p.trig;
+                if (stats) {
+                    if (!in_domain) atomicAdd(stats, (unsigned long long)nb);
+                    atomicAdd(stats + 1, (unsigned long long)nb);
+                }
+            }
+        }
+        return;
+    }
+    auto j0 = [](int k) { return NI * k; };  // interval k's first step
+    // the rows' constant slots, once: T slot NC + 1 = +inf (never counted), E slots 0 and NC + 1 NaN
+    for (int q = threadIdx.x; q < 4 * NI; q += 64 * (1 + NW)) {
+        sT[q / NI][q % NI][NC + 1] = __builtin_inff();
+        sE[q / NI][q % NI][0] = __builtin_nanf("");
+        sE[q / NI][q % NI][NC + 1] = __builtin_nanf("");
+    }
+
+    if (w > 0) {
+        const int el = (w - 1) * 64 + t;  // evaluator lane
+        // item q of interval k: e item (J, kc) = (q / NC, q % NC), q = el + EV u (u < NE)
+        float vq[RD][NE];
+        auto ld = [&](int k, float (&v)[NE]) __attribute__((always_inline)) {
+            const int kk = k <= ni ? k : ni;
+#pragma unroll
+            for (int u = 0; u < NE; u++) {
+                const int q = min(el + EV * u, NI * NC - 1);
+                v[u] = x[min(j0(kk) + q / NC + 1, n - 1)];  // the step the e is for
+            }
+        };
+        auto put = [&](int k, float phase_ref, const float (&v)[NE]) __attribute__((always_inline)) {
+            const int sl = k & 3;
+#pragma unroll
+            for (int u = 0; u < NE; u++) {
+                const int q = el + EV * u;
+                if (NE * EV > NI * NC && q >= NI * NC) break;
+                const int J = q / NC, kc = q % NC;
+                const double pr = pr_at(j0(k) + J);
+                const uint32_t cb = __builtin_bit_cast(uint32_t, (float)(pr + (double)phase_ref));
+                bool ok;
+                const float e = pred_e_cert(__builtin_bit_cast(float, cb - (uint32_t)HC + (uint32_t)kc), v[u],
+                                            pll_iv(v[u]), ok);
+                // a window that is not of positive finite floats never certifies: c0 < 2^126
+                const bool fin = cb > (uint32_t)HC && cb < 0x7F000000u;
+                sE[sl][J][kc + 1] = ok && fin ? e : __builtin_nanf("");
+            }
+#pragma unroll
+            for (int u = 0; u < NT; u++) {
+                const int q = el + EV * u;
+                if (NT * EV > NI * (NC + 1) && q >= NI * (NC + 1)) break;
+                const int J = q / (NC + 1), kc = q % (NC + 1);
+                const double pr = pr_at(j0(k) + J);
+                const uint32_t cb = __builtin_bit_cast(uint32_t, (float)(pr + (double)phase_ref));
+                sT[sl][J][kc] = phase_thr_exact(pr, cb - (uint32_t)HC + (uint32_t)kc);
+                if (kc == 0) sbase[sl][J] = cb - (uint32_t)HC - 1u;
+            }
+        };
+        // wave 1: interval k's trigArgs, bits(c_base) - 1 + the chain's count (the chain stored a
+        // redone interval itself)
+        auto store = [&](int k) {
+            if (w != 1) return;
+            const int sl = k & 3;
+            if (sexact[sl]) return;
+            if (t < NI) out[j0(k) + t] = __builtin_bit_cast(float, sbase[sl][t] + (uint32_t)srow[sl][t]);
+        };
+#pragma unroll
+        for (int u = 0; u < RD; u++) ld(1 + u, vq[(1 + u) % RD]);
+        put(1, p.phase, vq[1 % RD]);  // interval 1 from the phase at interval 0's start
+        ld(1 + RD, vq[1 % RD]);
+        __syncthreads();  // (prologue)
+        unsigned long long ev_body = 0, ev_wait = 0;
+        for (int i0 = 1; i0 <= ni; i0 += RD) {
+            unroll_ic(
+                [&](auto uc) {
+                    constexpr int u = decltype(uc)::value;
+                    constexpr int sl = (2 + u) % RD;  // slot of interval i + 1
+                    const int i = i0 + u;
+                    if (i <= ni) {
+                        const unsigned long long p0 = PROF_T();
+                        if (i + 1 <= ni) {
+                            put(i + 1, sst[(i - 1) & 3].y, vq[sl]);  // from the phase at interval i's start
+                            ld(i + 1 + RD, vq[sl]);
+                        }
+                        store(i - 1);
+                        const unsigned long long p1 = PROF_T();
+                        __syncthreads();
+                        ev_body += p1 - p0;
+                        ev_wait += PROF_T() - p1;
+                    }
+                },
+                std::make_integer_sequence<int, RD>{});
+        }
+        store(ni);
+#ifdef FMRX_AB_PROF
+        if (t == 0 && w == 1) {
+            atomicAdd(&g_cnt_prof[2], ev_body);
+            atomicAdd(&g_cnt_prof[3], ev_wait);
+        }
+#endif
+        (void)ev_body;
+        (void)ev_wait;
+        return;
+    }
+
+    // ---- the chain
+    PllCtx ctx{};
+    ctx.valid = false;
+    exact(p, ctx, 0, NI);  // interval 0 on the exact path
+    float integ = p.integ, phase = p.phase;
+    // the carry: the E row of the previous trigArg and its count (SGPR); after an exact stretch
+    // that trigArg's exact e in every lane
+    float cE;
+    uint32_t cC = 1;
+    auto carry_exact = [&](float a, int k) {
+        cE = exact_e(a, x[min(j0(k), n - 1)]);
+        cC = 1;
+    };
+    carry_exact((float)ctx.x, 1);
+    if (t == 0) {
+        sst[0] = make_float2(integ, phase);
+        sexact[0] = 1;
+    }
+    __syncthreads();  // (prologue)
+    unsigned long long n_redo = 0, n_inj = 0, ch_body = 0, ch_wait = 0;
+    const int ls = t < NP ? t : NP - 1;  // this lane's row slot (lanes past the row read its last)
+    for (int i = 1; i <= ni; i++) {
+        const unsigned long long p0 = PROF_T();
+        const int is = i & 3;
+        const float integ0 = integ, phase0 = phase;
+        int row = 0;
+        unroll_ic(
+            [&](auto hc) {
+                constexpr int H = decltype(hc)::value;
+                // the burst's rows before its steps
+                float T[CH], E[CH];
+#pragma unroll
+                for (int J = 0; J < CH; J++) {
+                    T[J] = sT[is][H * CH + J][ls];
+                    E[J] = sE[is][H * CH + J][ls];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                unroll_ic(
+                    [&](auto jc) {
+                        constexpr int J = decltype(jc)::value;
+                        // step H CH + J: e of the previous trigArg (filter.cpp:161-162)
+                        const float e = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cE), cC));
+                        const float2v kv = float2v{Ki, Kp} * e;
+                        integ = integ + kv.x;
+                        phase = phase + (kv.y + integ);
+                        // the count of thresholds the phase reaches: trigArg's place in the window + 1
+                        cC = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(phase >= T[J]));
+                        cE = E[J];
+                        int rw = row;
+                        const uint32_t sc = cC;
+                        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(rw) : "s"(sc), "i"(H * CH + J));
+                        row = rw;
+                    },
+                    std::make_integer_sequence<int, CH>{});
+            },
+            std::make_integer_sequence<int, NI / CH>{});
+        // the interval's verdict: no NaN e taken (the phase) or carried (the last trigArg's), the
+        // start state in pll_batch_fast's range; test hooks force misses
+        const float ce = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cE), cC));
+        const bool bad = !(phase == phase) || !(ce == ce) ||
+                         !(fabsf(phase0) < kPllMaxPhase && fabsf(integ0) < kPllMaxInteg) || i == min(miss, ni) ||
+                         i == inj;
+        if (bad) {  // uniform: redo the interval exactly from its start (the chain stores it)
+            n_redo++;
+            n_inj += i == inj ? 1 : 0;
+            const float a = (float)(pr_at(j0(i) - 1) + (double)phase0);  // the trigArg before it
+            PllState q;
+            PllCtx c{};
+            pll_state_at(q, c, integ0, phase0, trig0, (long long)j0(i), a, DeviceLib{});
+            exact(q, c, j0(i), j0(i) + NI);
+            integ = q.integ;
+            phase = q.phase;
+            carry_exact((float)c.x, i + 1);
+        }
+        if (t < NI) srow[is][t] = row;
+        sst[is] = make_float2(integ, phase);
+        sexact[is] = bad ? 1 : 0;
+        const unsigned long long p1 = PROF_T();
+        __syncthreads();
+        ch_body += p1 - p0;
+        ch_wait += PROF_T() - p1;
+    }
+#ifdef FMRX_AB_PROF
+    if (t == 0) {
+        atomicAdd(&g_cnt_prof[0], ch_body);
+        atomicAdd(&g_cnt_prof[1], ch_wait);
+        atomicAdd(&g_cnt_prof[4], (unsigned long long)ni);
+        atomicAdd(&g_cnt_prof[5], n_redo);
+    }
+#endif
+    (void)ch_body;
+    (void)ch_wait;
+    // the steps past the last interval exactly, from the end state
+    const long long jf = j0(ni + 1);
+    const float a = (float)(pr_at(jf - 1) + (double)phase);
+    PllState q;
+    PllCtx c{};
+    pll_state_at(q, c, integ, phase, trig0, jf, a, DeviceLib{});
+    exact(q, c, jf, n);
+    if (t == 0) {
+        S[0] = q.integ; S[1] = q.phase; S[2] = q.fbI; S[3] = q.fbQ; S[5] = q.trig;
+        if (stats) {
+            atomicAdd(stats, n_inj);  // "resumed": the inject hook's forced redos only
+            atomicAdd(stats + 1, (unsigned long long)nb);
+        }
+        if (redos) atomicAdd(&redos[kPllRedoForms * (size_t)s + (lo < kPllPipeMinLow ? 0 : lo < kPllPipeMin5 ? 1 : lo < kPllPipeMin ? 2 : 3)],
+                             (unsigned)n_redo);
+    }
 }
 
 }  // namespace
@@ -1338,6 +1659,10 @@ static void print_pred_prof() {
         std::fprintf(stderr, "pll_pred prof: batches %llu chain body %.1f wait %.1f, evaluator body %.1f wait %.1f "
                      "(shader cycles per batch)\n", h[4], (double)h[0] / h[4], (double)h[1] / h[4],
                      (double)h[2] / h[4], (double)h[3] / h[4]);
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_cnt_prof), sizeof h) == hipSuccess && h[4])
+        std::fprintf(stderr, "pll_cnt prof: intervals %llu chain body %.1f wait %.1f, evaluator body %.1f wait %.1f "
+                     "(shader cycles per interval), %llu redos\n", h[4], (double)h[0] / h[4], (double)h[1] / h[4],
+                     (double)h[2] / h[4], (double)h[3] / h[4], h[5]);
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_idx_prof), sizeof h) == hipSuccess && h[4])
         std::fprintf(stderr, "pll_idx prof: intervals %llu chain body %.1f wait %.1f, evaluator body %.1f wait %.1f "
                      "(shader cycles per interval), %llu redos\n", h[4], (double)h[0] / h[4], (double)h[1] / h[4],
@@ -1387,48 +1712,111 @@ void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_str
 
 void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
                      float* st, float* out, size_t ostride, int inject, int miss, int form,
-                     unsigned long long* stats) {
+                     unsigned long long* stats, unsigned* redos) {
 #ifdef FMRX_AB_PROF
     reg_pred_prof();
 #endif
     if (n <= 0) return;
     if (form == 22)
         hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8, 3>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
-                           stride, step, norm_bw, st, out, ostride, inject, miss, stats);
+                           stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
     else if (form == 21)
         hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
-                           stride, step, norm_bw, st, out, ostride, inject, miss, stats);
+                           stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
     else
         hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 1, 8, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
-                           stride, step, norm_bw, st, out, ostride, inject, miss, stats);
+                           stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
 }
 
-void launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
-                    float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats) {
-#ifdef FMRX_AB_PROF
-    reg_pred_prof();
-#endif
-    if (n <= 0) return;
-    static_assert(kPllIdxWaves == 4, "a CU a stream: the chain and the evaluators on its four SIMDs");
-    if (form == 17)
 #ifndef FMRX_IDX17_NC
 #define FMRX_IDX17_NC 32
+#endif
+#ifndef FMRX_IDX18_NC
+#define FMRX_IDX18_NC 32
 #endif
 #ifndef FMRX_IDX_NW
 #define FMRX_IDX_NW 4  // evaluator waves of the 32-candidate forms: two rows of candidates each
                        // (three waves: three rows, evaluator-bound; profiles/r04/ab_idx_nw4/)
 #endif
-        hipLaunchKernelGGL((pll_idx_kernel<FMRX_IDX17_NC, FMRX_IDX_NW>), dim3(n_streams), dim3(64 * (1 + FMRX_IDX_NW)), 0, s, io, n, n_streams, stride, step,
-                           norm_bw, st, out, ostride, inject, miss, 131072.0f, 262143.0f, stats);
-    else if (form == 18)
-#ifndef FMRX_IDX18_NC
-#define FMRX_IDX18_NC 32
+
+// A form's workgroup must be resident on one CU for its waves to run side by side (the chain
+// spins on barriers with its evaluators): checked once per kernel against the compiled register
+// and LDS use, so a build that outgrows it fails loudly instead of serialising.
+template <int NC, int NW>
+static int idx_launch(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step,
+                      float norm_bw, float* st, float* out, size_t ostride, int inject, int miss, float lo, float hi,
+                      unsigned long long* stats, unsigned* redos) {
+    constexpr int threads = 64 * (1 + NW);
+    static const int resident = [] {
+        int nb = 0;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pll_idx_kernel<NC, NW>, threads, 0) == hipSuccess
+                   ? nb : 0;
+    }();
+    if (resident < 1) return -1;
+    hipLaunchKernelGGL((pll_idx_kernel<NC, NW>), dim3(n_streams), dim3(threads), 0, s, io, n, n_streams, stride, step,
+                       norm_bw, st, out, ostride, inject, miss, lo, hi, stats, redos);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
+                   float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats,
+                   unsigned* redos) {
+#ifdef FMRX_AB_PROF
+    reg_pred_prof();
 #endif
-        hipLaunchKernelGGL((pll_idx_kernel<FMRX_IDX18_NC, FMRX_IDX_NW>), dim3(n_streams), dim3(64 * (1 + FMRX_IDX_NW)), 0, s, io, n, n_streams, stride, step,
-                           norm_bw, st, out, ostride, inject, miss, 262144.0f, 524287.0f, stats);
-    else
-        hipLaunchKernelGGL((pll_idx_kernel<16, 3>), dim3(n_streams), dim3(256), 0, s, io, n, n_streams, stride, step,
-                           norm_bw, st, out, ostride, inject, miss, 524288.0f, 1048575.0f, stats);
+    if (n <= 0) return 0;
+    if (form == 17)
+        return idx_launch<FMRX_IDX17_NC, FMRX_IDX_NW>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride,
+                                                      inject, miss, 131072.0f, 262143.0f, stats, redos);
+    if (form == 18)
+        return idx_launch<FMRX_IDX18_NC, FMRX_IDX_NW>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride,
+                                                      inject, miss, 262144.0f, 524287.0f, stats, redos);
+    return idx_launch<16, 3>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss, 524288.0f,
+                             1048575.0f, stats, redos);
+}
+
+// The count runner's forms (form: the trigOffset range as launch_pll numbers it), one stream a
+// workgroup of 1 + NW waves (a CU), residency checked like idx_launch.
+template <int NI, int NC, int NW>
+static int cnt_launch(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step,
+                      float norm_bw, float* st, float* out, size_t ostride, int inject, int miss, float lo, float hi,
+                      unsigned long long* stats, unsigned* redos) {
+    constexpr int threads = 64 * (1 + NW);
+    static const int resident = [] {
+        int nb = 0;
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, pll_cnt_kernel<NI, NC, NW>, threads, 0) == hipSuccess
+                   ? nb : 0;
+    }();
+    if (resident < 1) return -1;
+    hipLaunchKernelGGL((pll_cnt_kernel<NI, NC, NW>), dim3(n_streams), dim3(threads), 0, s, io, n, n_streams, stride,
+                       step, norm_bw, st, out, ostride, inject, miss, lo, hi, stats, redos);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int launch_pll_cnt(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
+                   float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats,
+                   unsigned* redos) {
+#ifdef FMRX_AB_PROF
+    reg_pred_prof();
+#endif
+    if (n <= 0) return 0;
+    switch (form) {
+        case 17:
+            return cnt_launch<16, 31, 4>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
+                                         131072.0f, 262143.0f, stats, redos);
+        case 18:
+            return cnt_launch<16, 31, 4>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
+                                         262144.0f, 524287.0f, stats, redos);
+        case 19:
+            return cnt_launch<32, 15, 4>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
+                                         524288.0f, 1048575.0f, stats, redos);
+        case 20:
+            return cnt_launch<64, 15, 4>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
+                                         kPllPipeMinLow, kPllPipeMin5 - 1.0f, stats, redos);
+        default:
+            return cnt_launch<64, 7, 4>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
+                                        kPllPipeMin5, kPllPipeMin - 1.0f, stats, redos);
+    }
 }
 
 }  // namespace fmrx

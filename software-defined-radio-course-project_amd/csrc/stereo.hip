@@ -864,16 +864,12 @@ inline int ok() { return hipGetLastError() == hipSuccess ? 0 : -2; }
 
 }  // namespace
 
-int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s) {
+int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s, bool tiled) {
     if (L.n_if <= 0) return 0;
     if (L.bp_taps > kBpMax) return -1;
     BpTaps t{};
     for (int k = 0; k < L.bp_taps; k++) t.c[k] = make_float2(L.ch_c[k], L.ca_c[k]);
     const dim3 grid((L.n_if + 255) / 256, n_streams), block(256);
-    static const bool tiled = [] {  // FMRX_BPF_TILE=0: the per-output kernel (A/B measurements)
-        const char* e = std::getenv("FMRX_BPF_TILE");
-        return !(e && e[0] == '0');
-    }();
     if (L.bp_taps == 51 && L.hist >= 50 && tiled)
         hipLaunchKernelGGL(bpf_pair_tile_kernel<51>, dim3((L.n_if + kBpTile - 1) / kBpTile, n_streams), dim3(kBpThreads),
                            0, s, L, t);
@@ -926,29 +922,18 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     int* fail = reinterpret_cast<int*>(rec + rb * (size_t)n_streams);
     // one stream per wave while the waves fit one per SIMD, then more streams per wave
     const int n_simd = hint.n_simd;
-    const bool spec_env = [] {  // read per call: tests switch it within one process
-        const char* e = std::getenv("FMRX_PLL_SPEC");
-        return !(e && e[0] == '0');
-    }();
-    // test hook (tests/test_gpu_parity.py): the runners corrupt batch 1 + (k + s) % (nb - 1) of
-    // stream s (the three-wave runner: a forced miss on one interval), so the check and the
-    // fix-up from that batch (the exact redo) run on every stream
-    const int inject = [] {
-        const char* e = std::getenv("FMRX_PLL_SPEC_INJECT");
-        return e ? std::atoi(e) : -1;
-    }();
+    const PllKnobs& kn = hint.knobs;  // the context's switches (fmrx_debug_set_knob)
+    const bool spec_env = kn.spec != 0;
+    // test hook (tests/test_gpu_parity.py, knob pll_inject): the runners corrupt batch
+    // 1 + (k + s) % (nb - 1) of stream s (the self-certifying runners: a forced miss on one
+    // interval), so the check and the fix-up from that batch (the exact redo) run on every stream
+    const int inject = kn.inject;
     const bool spec = spec_env && (reinterpret_cast<uintptr_t>(io) & 15) == 0 && stride % 4 == 0;
-    // FMRX_PLL_SAT=0 / FMRX_PLL_PRED=0 (measurements, tests): saturated segments / segments from
-    // 2^20 steps on the ordinary runner too
-    const int sat_ok = [] {
-        const char* e = std::getenv("FMRX_PLL_SAT");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    // (FMRX_PLL_PRED=2, tests: the two-wave runner even where its waves share SIMDs)
-    const int pred_ok = [] {
-        const char* e = std::getenv("FMRX_PLL_PRED");
-        return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
-    }();
+    // pll_sat = 0 / pll_pred = 0 (measurements, tests): saturated segments / segments from 2^20
+    // steps on the ordinary runner too (pll_pred = 2, tests: the two-wave runner even where its
+    // waves share SIMDs)
+    const int sat_ok = kn.sat != 0 ? 1 : 0;
+    const int pred_ok = kn.pred == 0 ? 0 : kn.pred == 2 ? 2 : 1;
     int spw = 1;
     while (spw < 64 && (long long)spw * n_simd < n_streams) spw *= 2;
     // Waves of 64 lanes; past 256 waves, workgroups of 4 waves, one per SIMD of a CU: 64-lane
@@ -957,24 +942,15 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     const int wpg = waves > n_simd / 4 ? 4 : 1;
     const dim3 grid((waves + wpg - 1) / wpg), block(64 * wpg);
 
-    // FMRX_PLL_PIPE=0 (measurements, tests): no three-wave runner; FMRX_PLL_PIPE_MISS=k (test
-    // hook): its check reports a miss on interval k of every launch, so the redo path runs
-    const int pipe_env = [] {
-        const char* e = std::getenv("FMRX_PLL_PIPE");
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    const int pipe_miss = [] {
-        const char* e = std::getenv("FMRX_PLL_PIPE_MISS");
-        return e ? std::atoi(e) : -1;
-    }();
-    // FMRX_PLL_HINT_SKEW=d (test hook): the host's trigOffset bounds shifted by d samples, so the
+    // pll_pipe = 0 (measurements, tests): no three-wave runner; pll_pipe_miss = k (test hook): the
+    // self-certifying runners report a miss on interval k of every launch, so the redo path runs
+    const int pipe_env = kn.pipe != 0 ? 1 : 0;
+    const int pipe_miss = kn.pipe_miss;
+    // pll_hint_skew = d (test hook): the host's trigOffset bounds shifted by d samples, so the
     // runners launched are the wrong ones.  A segment stream no runner takes keeps the pre-pass's
-    // fail[] sentinel 0 and is resumed whole on the certified path; a three-wave launch outside its
-    // domain runs its range exactly (same bits either way)
-    const double skew = [] {
-        const char* e = std::getenv("FMRX_PLL_HINT_SKEW");
-        return e ? std::atof(e) : 0.0;
-    }();
+    // fail[] sentinel 0 and is resumed whole on the certified path; a self-certifying launch outside
+    // its domain runs its range exactly (same bits either way)
+    const double skew = kn.skew;
     // filter.cpp:163: 2*PI*(freq/Fs) in double from the float quotient (host == device IEEE)
     const double step = (2.0 * 3.14159265358979323846) * static_cast<double>(freq / fs);  // dy4.h:14 PI
     const bool step_ok = std::fabs(step * (double)kPllTrigStick) < kPllMaxPr;
@@ -989,13 +965,10 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     // the three-wave runner: every stream at the same known trigOffset t, a SIMD per wave (one
     // stream a workgroup of three); it takes the samples from trigOffset 2^20 on
     const bool pipe = spec && pred_ok && pipe_env && spw == 1 && 3 * n_streams <= n_simd && k && hlo == hhi;
-    // the index runner in [2^17, 2^20) wants four SIMDs a stream (FMRX_PLL_IDX=0: not launched;
-    // FMRX_PLL_IDX=1: from 2^18 only, the lane runner keeping [2^17, 2^18))
-    const int idx_env = [] {
-        const char* e = std::getenv("FMRX_PLL_IDX");
-        return (e && e[0] == '0') ? 0 : (e && e[0] == '1') ? 1 : 2;
-    }();
-    const bool idx = pipe && idx_env && kPllIdxWaves * n_streams <= n_simd;
+    // the index runner in [2^17, 2^20) wants a CU a stream (pll_idx = 0: not launched; 1: from
+    // 2^18 only, the lane runner keeping [2^17, 2^18))
+    const int idx_env = kn.idx == 0 ? 0 : kn.idx == 1 ? 1 : 2;
+    const bool idx = pipe && idx_env && kPllIdxSimds * n_streams <= n_simd;
     const double fast_min = idx ? (double)(idx_env == 2 ? kPllIdxMin64 : kPllIdxMin) : (double)kPllPipeMinLow;
     size_t n_seg = (size_t)n;  // samples through the segment loop
     if (pipe) n_seg = hlo >= fast_min ? 0 : std::min((size_t)n, (size_t)(fast_min - hlo));
@@ -1076,6 +1049,7 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     // [2^19, 2^20) forms (64 / 32 / 16 candidates), then the three-wave runner's [2^20, 2^21)
     // 16-step five-candidate form, [2^21, 2^22) the 64-step one, from 2^22 (the stick included)
     // three candidates
+    int idx_rc = 0;
     for (size_t j = n_seg; pipe && j < (size_t)n;) {
         const double t = std::min(hlo + (double)j, (double)kPllTrigStick);
         const int form = t < 262144.0 ? 17 : t < 524288.0 ? 18 : t < (double)kPllPipeMinLow ? 19
@@ -1086,12 +1060,15 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         const int kind = form == 17 ? kStIdx17 : form == 18 ? kStIdx18 : form == 19 ? kStIdx19
                        : form == 20 ? kStPipe20 : form == 21 ? kStPipe21 : kStPipe22;
         timed(kind, (double)(e - j), [&] {
-            if (form < 20)
-                launch_pll_idx(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j, (size_t)n,
-                               inject, pipe_miss, form, spec_stats);
+            if (form < 22 && ((kn.cnt >> (form - 17)) & 1) && kPllIdxSimds * n_streams <= n_simd)
+                idx_rc |= launch_pll_cnt(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j,
+                                         (size_t)n, inject, pipe_miss, form, spec_stats, hint.redos);
+            else if (form < 20)
+                idx_rc |= launch_pll_idx(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j,
+                                         (size_t)n, inject, pipe_miss, form, spec_stats, hint.redos);
             else
                 launch_pll_pipe(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j, (size_t)n,
-                                inject, pipe_miss, form, spec_stats);
+                                inject, pipe_miss, form, spec_stats, hint.redos);
         });
         j = e;
     }
@@ -1105,7 +1082,7 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         (void)hipMemcpy2DAsync(reinterpret_cast<float*>(side + 4 * seg * (size_t)n_streams), (size_t)n * sizeof(float),
                                io, stride * sizeof(float), (size_t)n * sizeof(float), n_streams,
                                hipMemcpyDeviceToDevice, s);
-    return ok();
+    return idx_rc ? -2 : ok();
 }
 
 int launch_pll_nco(float* io, int n, int n_streams, size_t stride, float nco_scale, float phase_adjust, float* st,

@@ -195,6 +195,7 @@ def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, dev
     nb = int(seconds * geo.rf_fs * 2 // bb)
     pcm_len = nb * geo.pcm_samples
     t_synth = [0.0]
+    redos = [None]  # this rank's streams x 4 redone intervals (fmrx_debug_pll_redos), warm-up call
 
     def setup():
         rx = fmrx.Receiver(mode, fmrx.STEREO, n_streams=max(1, len(ids)), device=device)
@@ -208,8 +209,14 @@ def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, dev
                 rx.synchronize()
             t_synth[0] = time.perf_counter() - t
             if ids and warmup:
+                # the untimed warm-up call does the timed call's work exactly (same input, same
+                # power-on state): the runners' per-stream redo counts are taken here
+                redo = torch.zeros((len(ids), 4), dtype=torch.int32, device=dev)
+                rx.debug_pll_redos(redo.data_ptr())
                 rx.process_device(iq.data_ptr(), nb, out.data_ptr())
                 rx.synchronize()
+                rx.debug_pll_redos(None)
+                redos[0] = redo.cpu().numpy()
                 rx.reset()
         except Exception:
             rx.close()
@@ -253,10 +260,25 @@ def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, dev
                         for r, v in enumerate(res["per_rank"])]}
     if "post" in res:
         out["latency"] = res["post"]
+    if redos[0] is not None and len(ids):
+        # rank 0's shard: the streams whose redone intervals (a trigArg outside the runner's
+        # candidates) cost the most serial time -- the slowest of them sets the call's wall time
+        r = redos[0]
+        tot = r.sum(axis=1)
+        worst = [int(i) for i in tot.argsort()[::-1][:8]]
+        out["redos"] = {"streams": len(ids), "forms": ["index", "pipe16", "pipe64_five", "pipe_three"],
+                        "total_per_form": [int(x) for x in r.sum(axis=0)],
+                        "max_per_form": [int(x) for x in r.max(axis=0)],
+                        "worst_streams": [{"stream": ids[i], "redos": [int(x) for x in r[i]]} for i in worst],
+                        "source": "fmrx_debug_pll_redos over the untimed warm-up call (same input, same state)"}
     if expect:
-        got = {sid: hashlib.sha256(gathered[sid].cpu().numpy().tobytes()).hexdigest() for sid in expect}
+        host = gathered.cpu().numpy()
+        got = {sid: hashlib.sha256(host[sid].tobytes()).hexdigest() for sid in expect}
         out["checked_streams"] = sorted(expect)
-        out["bit_exact_vs_reference"] = all(got[sid] == expect[sid] for sid in expect)
+        bad = sorted(sid for sid in expect if got[sid] != expect[sid])
+        out["bit_exact_vs_reference"] = not bad
+        if bad:
+            out["mismatched_streams"] = bad
     else:
         out["parity"] = f"unpinned: no reference hashes recorded for {n_streams} streams x {nb} blocks"
     return out

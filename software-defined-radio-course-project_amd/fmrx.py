@@ -87,6 +87,8 @@ PROTOTYPES = {
     "fmrx_test_pll_fallback": (C.c_int, [_vp, C.c_int, _vp, _vp, _sz, _vp]),
     "fmrx_debug_mono_stamps": (C.c_int, [_vp, _vp, _sz, C.POINTER(_sz)]),
     "fmrx_debug_pll_stats": (C.c_int, [_vp, _vp]),
+    "fmrx_debug_set_knob": (C.c_int, [_vp, C.c_int, C.c_double]),
+    "fmrx_debug_pll_redos": (C.c_int, [_vp, _vp]),
     "fmrx_debug_stage_timing": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                           C.POINTER(C.c_long), C.c_int]),
 }
@@ -95,6 +97,15 @@ PROTOTYPES = {
 STAGES = ["front_end", "bandpass_pair", "pll_prep", "runner_lane", "runner_pred", "runner_sat", "runner_pipe20",
           "runner_pipe21", "runner_pipe22", "pll_check", "pll_tail", "pll_nco", "audio", "runner_idx17", "runner_idx18",
           "runner_idx19"]
+
+# fmrx_debug_set_knob's knobs (include/fmrx.h FMRX_KNOB_*): none changes the output; the
+# pll_inject / pll_pipe_miss / pll_hint_skew test hooks make the PLL runners redo work
+KNOBS = {"pll_spec": 0, "pll_sat": 1, "pll_pred": 2, "pll_pipe": 3, "pll_idx": 4, "stereo_chunks": 5,
+         "mono_split": 6, "bpf_tile": 7, "halo_kernel": 8, "pll_inject": 9, "pll_pipe_miss": 10,
+         "pll_hint_skew": 11, "pll_cnt": 12}
+# knobs every new Receiver applies after fmrx_create (tests set it per test, e.g. with
+# monkeypatch.setattr; the library itself reads only the tuning knobs' environment variables)
+DEFAULT_KNOBS: dict = {}
 
 _lib = None
 
@@ -173,7 +184,7 @@ class Receiver:
     """
 
     def __init__(self, mode: int = 0, channels: int = MONO, rf_taps: int = 51, n_streams: int = 1,
-                 device: int = 0, bp_taps: int = 51, audio_taps: int = 51):
+                 device: int = 0, bp_taps: int = 51, audio_taps: int = 51, knobs: dict | None = None):
         self.cfg = default_config(mode, channels, rf_taps=rf_taps, n_streams=n_streams,
                                   device=device, bp_taps=bp_taps, audio_taps=audio_taps)
         self.geo = geometry(self.cfg)
@@ -182,6 +193,12 @@ class Receiver:
         self.h = h
         self.n_streams = n_streams
         self.channels = channels
+        for k, v in {**DEFAULT_KNOBS, **(knobs or {})}.items():
+            self.set_knob(k, v)
+
+    def set_knob(self, name: str, value: float) -> None:
+        """fmrx_debug_set_knob (include/fmrx.h FMRX_KNOB_*; KNOBS names them)."""
+        _check(lib().fmrx_debug_set_knob(self.h, KNOBS[name], float(value)))
 
     def close(self) -> None:
         if getattr(self, "h", None):
@@ -381,6 +398,11 @@ class Receiver:
         """Diagnostic speculative-PLL counters (fmrx.h): d_counts[0] += runner batches that did
         not verify, d_counts[1] += batches checked (2 u64 on the device); None turns it off."""
         _check(lib().fmrx_debug_pll_stats(self.h, d_counts))
+
+    def debug_pll_redos(self, d_counts) -> None:
+        """fmrx_debug_pll_redos: per-stream redone intervals of the self-certifying runners
+        (n_streams x 4 u32 on the device, zeroed by the caller; None turns it off)."""
+        _check(lib().fmrx_debug_pll_redos(self.h, d_counts))
 
 
 def build() -> None:

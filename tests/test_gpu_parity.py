@@ -23,6 +23,12 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
+
+def knobs(monkeypatch, fm, **kw):
+    """Knobs (fmrx_debug_set_knob) of the Receivers this test creates; the test hooks among them
+    (pll_inject, pll_pipe_miss, pll_hint_skew) are not readable from the environment."""
+    monkeypatch.setattr(fm, "DEFAULT_KNOBS", {**fm.DEFAULT_KNOBS, **kw})
+
 def sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
@@ -189,7 +195,7 @@ def test_trig_hint_after_set_state(fmrx, monkeypatch):
     """The host-side trigOffset bounds that pick which PLL runners launch (api.cpp TrigTrack)
     follow a restored blob: a stream restored at 2^20 - 2,000 crosses into the predicted
     runner's range within the call and one at 2^24 - 3,000 into the saturated runner's; the PCM
-    equals the lane runner's alone (FMRX_PLL_PRED=0, FMRX_PLL_SAT=0: every segment on it), and
+    equals the lane runner's alone (knob pll_pred=0, knob pll_sat=0: every segment on it), and
     every batch verified -- a runner left out by a wrong bound would leave its waves unrun."""
     bb = oracle.MODES[0][0]
     iq = iqgen.make("synth:91", 30 * bb)
@@ -212,11 +218,10 @@ def test_trig_hint_after_set_state(fmrx, monkeypatch):
     for trig in (1048576.0 - 2000, 16777216.0 - 3000):
         got, (resumed, checked) = run(trig)
         assert checked > 0 and resumed == 0, (trig, resumed, checked)
-        monkeypatch.setenv("FMRX_PLL_PRED", "0")
-        monkeypatch.setenv("FMRX_PLL_SAT", "0")
+        knobs(monkeypatch, fmrx, pll_pred=0)
+        knobs(monkeypatch, fmrx, pll_sat=0)
         want, _ = run(trig)
-        monkeypatch.delenv("FMRX_PLL_PRED")
-        monkeypatch.delenv("FMRX_PLL_SAT")
+        knobs(monkeypatch, fmrx, pll_pred=1, pll_sat=1)
         assert np.array_equal(got, want), trig
 
 
@@ -324,9 +329,9 @@ def test_unequal_wave_shares_multistream(fmrx, orc, monkeypatch, channels, n_str
     """The fused kernel's two-waves-per-SIMD split (mono_fused.hip mono_share: workgroups w and
     w + grid/2 share a span, the first taking kOlderShare/1024 of it) with several streams:
     ~2,048 workgroups (3 streams: 682 even segments each, 2,046 workgroups), an extreme share
-    (FMRX_MONO_SPLIT=900), and the stereo engine's front end.  Every stream equals the oracle."""
+    (knob mono_split=900), and the stereo engine's front end.  Every stream equals the oracle."""
     if share is not None:
-        monkeypatch.setenv("FMRX_MONO_SPLIT", share)
+        knobs(monkeypatch, fmrx, mono_split=float(share))
     nb, bb = 420, 12800  # 2,800 chunks per stream: enough for the full-chip grid
     recipes = [("synth:%d" if s % 2 == 0 else "rand:%d") % (300 + s) for s in range(n_streams)]
     ins = np.stack([iqgen.make(r, nb * bb) for r in recipes])
@@ -487,11 +492,11 @@ def test_stereo_pipelined_chunks(fmrx, orc, monkeypatch, mode, n_streams, nb, ch
     """The pipelined stereo engine (api.cpp run_stereo_pipelined): a call's blocks in chunks,
     front end + band-pass of chunk k + 1 and audio of chunk k - 1 on their own HIP streams beside
     the PLL of chunk k, every chunk reading the call's buffers at its offset (a chunk's RF halo
-    is the call's own bytes in front of it).  FMRX_STEREO_CHUNKS forces the chunk count (None: the
+    is the call's own bytes in front of it).  knob stereo_chunks forces the chunk count (None: the
     default, 8 from 16 streams, fewer when a chunk would hold < 2^14 samples); two calls in a row
     check the carried state.  Modes 0/1 take the tiled audio kernel, mode 2 the per-frame one."""
     if chunks is not None:
-        monkeypatch.setenv("FMRX_STEREO_CHUNKS", chunks)
+        knobs(monkeypatch, fmrx, stereo_chunks=float(chunks))
     bb = oracle.MODES[mode][0]
     rf_fs = oracle.MODES[mode][3]
     recipes = [("synth:%d" if s % 3 else "rand:%d") % (500 + s) for s in range(n_streams)]
@@ -509,7 +514,7 @@ def test_stereo_pipelined_checkpoint_resume(fmrx, orc, monkeypatch):
     tail, mono delay; api.cpp run_stereo_pipelined) through a checkpoint: 16 streams (the
     engine's default threshold) in pipelined calls, the blob into a second context, which goes
     on pipelined, bit-exact against the oracle on three streams."""
-    monkeypatch.setenv("FMRX_STEREO_CHUNKS", "3")
+    knobs(monkeypatch, fmrx, stereo_chunks=3)
     ns, nb, bb = 16, 30, 12800
     iq = np.stack([iqgen.make(f"synth:{620 + k}", 2 * nb * bb) for k in range(ns)])
     with fmrx.Receiver(0, fmrx.STEREO, n_streams=ns) as rx:
@@ -540,18 +545,17 @@ def test_many_streams_cross_wave_boundaries(fmrx, orc, channels, n_streams):
         assert np.array_equal(out[s], orc.run(0, 51, ins[s], [field])[field]), s
 
 
-@pytest.mark.parametrize("env", [{"FMRX_PLL_SPEC": "0"}, {"FMRX_PLL_SPEC_INJECT": "0"},
-                                 {"FMRX_PLL_SPEC_INJECT": "7"}])
+@pytest.mark.parametrize("env", [{"pll_spec": "0"}, {"pll_inject": "0"},
+                                 {"pll_inject": "7"}])
 @pytest.mark.parametrize("n_streams,nb", [(1, 450), (6, 40), (1100, 2)])
 def test_pll_speculation_fallbacks(fmrx, orc, monkeypatch, env, n_streams, nb):
     """The speculative PLL (stereo.hip pll_spec_kernel -> pll_check_kernel -> pll_kernel from
     the first batch that differs) equals the reference whatever the runner got wrong: with the
-    test hook FMRX_PLL_SPEC_INJECT=k the runner corrupts batch 1 + (k + s) % (nb - 1) of every
+    test hook knob pll_inject=k the runner corrupts batch 1 + (k + s) % (nb - 1) of every
     stream s, so every stream resumes at its own batch (and a wave of several streams, at 1,100
-    streams, at the earliest of them); FMRX_PLL_SPEC=0 is the plain certified launch.  450
+    streams, at the earliest of them); knob pll_spec=0 is the plain certified launch.  450
     blocks cross the 2^18-sample segment boundary."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    knobs(monkeypatch, fmrx, **{k: float(v) for k, v in env.items()})
     bb = 12800
     recipes = [("synth:%d" if s % 3 else "rand:%d") % (900 + s) for s in range(n_streams)]
     ins = np.stack([iqgen.make(r, nb * bb) for r in recipes])
@@ -563,7 +567,7 @@ def test_pll_speculation_fallbacks(fmrx, orc, monkeypatch, env, n_streams, nb):
         if n_streams == 1:
             out2 = np.atleast_2d(rx.process(ins))  # a second call from the carried state
     resumed, checked = counts.cpu().tolist()
-    if "FMRX_PLL_SPEC_INJECT" in env:  # every stream's corrupted batch was caught and resumed
+    if "pll_inject" in env:  # every stream's corrupted batch was caught and resumed
         assert checked > 0 and resumed >= n_streams, (resumed, checked)
     else:  # the plain launch: nothing speculative ran
         assert (resumed, checked) == (0, 0)
@@ -577,11 +581,11 @@ def test_pll_speculation_fallbacks(fmrx, orc, monkeypatch, env, n_streams, nb):
 @pytest.mark.parametrize("skew", [4194304.0, 1048576.0, 16777216.0])
 def test_pll_wrong_hint_fails_safe(fmrx, orc, monkeypatch, skew):
     """The host picks a segment's runners from its trigOffset bounds (api.cpp TrigTrack).  With
-    the bounds deliberately wrong (test hook FMRX_PLL_HINT_SKEW: the host believes the streams
+    the bounds deliberately wrong (test hook knob pll_hint_skew: the host believes the streams
     are `skew` samples further on), the runners launched leave the streams alone; the pre-pass's
     fail[] sentinel (0) then makes pll_kernel resume each such stream's whole segment on the
     certified path: slower, bit-identical (stats: every checked batch resumed)."""
-    monkeypatch.setenv("FMRX_PLL_HINT_SKEW", str(skew))
+    knobs(monkeypatch, fmrx, pll_hint_skew=skew)
     nb, bb, n_streams = 30, 12800, 3
     ins = np.stack([iqgen.make(f"synth:{950 + s}", nb * bb) for s in range(n_streams)])
     with fmrx.Receiver(0, fmrx.STEREO, n_streams=n_streams) as rx:
@@ -771,10 +775,10 @@ def test_pll_saturated_runner(fmrx, orc, monkeypatch, inject, sat, pipe, freq, n
     two-wave predicted runner; and a corrupted runner batch (check + certified resume).  The
     speculation counters must show every batch verified without the corruption -- a runner
     that disagrees with the exact path would otherwise pass here, fixed up by the resume."""
-    monkeypatch.setenv("FMRX_PLL_SAT", sat)
-    monkeypatch.setenv("FMRX_PLL_PIPE", pipe)
+    knobs(monkeypatch, fmrx, pll_sat=float(sat))
+    knobs(monkeypatch, fmrx, pll_pipe=float(pipe))
     if inject is not None:
-        monkeypatch.setenv("FMRX_PLL_SPEC_INJECT", inject)
+        knobs(monkeypatch, fmrx, pll_inject=float(inject))
     n = 20000
     rng = np.random.default_rng(24)
     t = np.arange(n)
@@ -803,16 +807,16 @@ def test_pll_saturated_runner(fmrx, orc, monkeypatch, inject, sat, pipe, freq, n
 def test_pll_predicted_runner(fmrx, orc, monkeypatch, trig0, inject, pred, pipe):
     """Segments from trigOffset 2^20 up to the 2^24 stick: the predicted-trigArg runners
     (pll_pred.hip: three waves one stream a workgroup -- five candidates in 16-step intervals from
-    2^20, in 64-step ones from 2^21, three candidates from 2^22; FMRX_PLL_PIPE=0: the two-wave
-    runner throughout; FMRX_PLL_PRED=0: the lane runner), starting at 2^20, at 2^21 + 33, 100 steps
+    2^20, in 64-step ones from 2^21, three candidates from 2^22; knob pll_pipe=0: the two-wave
+    runner throughout; knob pll_pred=0: the lane runner), starting at 2^20, at 2^21 + 33, 100 steps
     below 2^22 (its form runs on past it), at 2^22 + 17, and 5,000 steps below the stick (its pr
     stops rising inside the segment); 2^20 - 1 runs its first step on the index runner's
-    [2^19, 2^20) form (pll_idx_kernel; the lane runner with FMRX_PLL_PIPE=0).  A corrupted batch
+    [2^19, 2^20) form (pll_idx_kernel; the lane runner with knob pll_pipe=0).  A corrupted batch
     must be caught and resumed; without it every batch verifies."""
-    monkeypatch.setenv("FMRX_PLL_PRED", pred)
-    monkeypatch.setenv("FMRX_PLL_PIPE", pipe)
+    knobs(monkeypatch, fmrx, pll_pred=float(pred))
+    knobs(monkeypatch, fmrx, pll_pipe=float(pipe))
     if inject is not None:
-        monkeypatch.setenv("FMRX_PLL_SPEC_INJECT", inject)
+        knobs(monkeypatch, fmrx, pll_inject=float(inject))
     n = 20000
     rng = np.random.default_rng(int(trig0) % 1000)
     t = np.arange(n)
@@ -839,13 +843,13 @@ def test_pll_predicted_runner(fmrx, orc, monkeypatch, trig0, inject, pred, pipe)
 @pytest.mark.parametrize("trig0", [1048600.0, 2097185.0, 4194321.0, 16772216.0, 16777216.0])
 @pytest.mark.parametrize("miss", ["1", "2", "150", "311", "312", "1248", "5000"])
 def test_pll_pipe_redo(fmrx, orc, monkeypatch, trig0, miss):
-    """The three-wave runner's miss path (pll_pipe_kernel): FMRX_PLL_PIPE_MISS=k makes its check
+    """The three-wave runner's miss path (pll_pipe_kernel): knob pll_pipe_miss=k makes its check
     report interval k as missed (past the last interval: the last), so the chain redoes that
     interval and the two after it exactly and the evaluators restart from the corrected phase.
     20,000 steps = batch 0 + 312 intervals of 64 steps + 1 batch from 2^21 (k = 1, 150, 311 and
     312: the first, a middle one and the verdicts read after the loop), batch 0 + 1,249 intervals
     of 16 steps in [2^20, 2^21) (1,248 and 1,249 the last two).  Bit-exact, every batch verifies."""
-    monkeypatch.setenv("FMRX_PLL_PIPE_MISS", miss)
+    knobs(monkeypatch, fmrx, pll_pipe_miss=float(miss))
     n = 20000
     rng = np.random.default_rng(int(trig0) % 977)
     t = np.arange(n)
@@ -873,19 +877,19 @@ def test_pll_pipe_redo(fmrx, orc, monkeypatch, trig0, miss):
 def test_pll_index_runner(fmrx, orc, monkeypatch, trig0, inject, idx):
     """trigOffset in [2^17, 2^20): the index runner (pll_pred.hip pll_idx_kernel: the chain forms
     trigArg itself and reads its e from a lane of a candidate row -- 32 candidates from 2^17 and
-    from 2^18, 16 from 2^19; FMRX_PLL_IDX=1: from 2^18 only, the lane runner below), starting at
-    2^17 (the default, FMRX_PLL_IDX=2 or unset, starts there; with 1 the lane runner hands over at
+    from 2^18, 16 from 2^19; knob pll_idx=1: from 2^18 only, the lane runner below), starting at
+    2^17 (the default, knob pll_idx=2 or unset, starts there; with 1 the lane runner hands over at
     2^18), at 2^18 + 33, 100 steps below 2^19 (the 2^18 form hands over to the 2^19 one
     inside the call), at 600,000, and 5,000 steps below 2^20 (the three-wave runner takes over);
-    125,000 starts on the lane runner and crosses into it.  FMRX_PLL_IDX=0: the lane runner below
+    125,000 starts on the lane runner and crosses into it.  knob pll_idx=0: the lane runner below
     2^20.  Bit-exact against the oracle; a forced miss
-    (FMRX_PLL_SPEC_INJECT) is redone exactly, and without it no batch is."""
+    (knob pll_inject) is redone exactly, and without it no batch is."""
     if idx is None:
-        monkeypatch.delenv("FMRX_PLL_IDX", raising=False)
+        knobs(monkeypatch, fmrx, pll_idx=2)
     else:
-        monkeypatch.setenv("FMRX_PLL_IDX", idx)
+        knobs(monkeypatch, fmrx, pll_idx=float(idx))
     if inject is not None:
-        monkeypatch.setenv("FMRX_PLL_SPEC_INJECT", inject)
+        knobs(monkeypatch, fmrx, pll_inject=float(inject))
     n = 20000
     rng = np.random.default_rng(int(trig0) % 1009)
     t = np.arange(n)
@@ -911,11 +915,11 @@ def test_pll_index_runner(fmrx, orc, monkeypatch, trig0, inject, idx):
 @pytest.mark.parametrize("trig0", [131100.0, 300000.0, 700000.0])
 @pytest.mark.parametrize("miss", ["1", "2", "600", "1248", "1249", "5000"])
 def test_pll_index_redo(fmrx, orc, monkeypatch, trig0, miss):
-    """The index runner's miss path: FMRX_PLL_PIPE_MISS=k makes its check report interval k as
+    """The index runner's miss path: knob pll_pipe_miss=k makes its check report interval k as
     missed (past the last: the last), so the chain redoes it and the two after it exactly and the
     evaluators restart from the corrected phase.  20,000 steps = interval 0 + 1,249 intervals of
     16 steps + a tail (1,248 and 1,249: the verdicts read after the loop).  Bit-exact."""
-    monkeypatch.setenv("FMRX_PLL_PIPE_MISS", miss)
+    knobs(monkeypatch, fmrx, pll_pipe_miss=float(miss))
     n = 20000
     rng = np.random.default_rng(int(trig0) % 983)
     t = np.arange(n)
@@ -940,15 +944,15 @@ def test_pll_index_redo(fmrx, orc, monkeypatch, trig0, miss):
 def test_index_runner_streams(fmrx, monkeypatch):
     """pll_idx_kernel over many streams (200: four waves each still fit the SIMDs), every stream
     put at trigOffset 2^18 - 4,000 through the state blob (the runners need the streams at one
-    known trigOffset: the 2^17 form hands over to the 2^18 one inside the call; FMRX_PLL_IDX=1:
+    known trigOffset: the 2^17 form hands over to the 2^18 one inside the call; knob pll_idx=1:
     the lane runner to 2^18), 24 blocks in one call: the PCM equals the same call with the index
-    runner off (FMRX_PLL_IDX=0: the lane runner, checked by pll_check_kernel), and no batch is
+    runner off (knob pll_idx=0: the lane runner, checked by pll_check_kernel), and no batch is
     redone."""
     ns, nb, bb = 200, 24, 12800
     ins = np.stack([iqgen.make("synth:%d" % (700 + s % 5), (nb + 2) * bb) for s in range(ns)])
     outs = []
     for idx in ("2", "1", "0"):
-        monkeypatch.setenv("FMRX_PLL_IDX", idx)
+        knobs(monkeypatch, fmrx, pll_idx=float(idx))
         with fmrx.Receiver(0, fmrx.STEREO, n_streams=ns) as rx:
             rx.process(ins[:, : 2 * bb])
             blob = bytearray(rx.get_state())
@@ -967,24 +971,30 @@ def test_index_runner_streams(fmrx, monkeypatch):
     assert np.array_equal(outs[0], outs[2]) and np.array_equal(outs[1], outs[2])
 
 
-def test_pipe_runner_streams(fmrx, monkeypatch):
+@pytest.mark.parametrize("mixed", [False, True])
+def test_pipe_runner_streams(fmrx, monkeypatch, mixed):
     """pll_pipe_kernel over many streams (300: three waves each still fit the SIMDs), every
     stream put at trigOffset 2^22 - 6,000 through the state blob (the runners need the streams at
     one known trigOffset: the 2^21 form hands over to the 2^22 one inside the call), 24 blocks in
     one call: every batch verifies, and the PCM equals the same call with the three-wave runner
-    off (FMRX_PLL_PIPE=0: the two-wave runner, checked by pll_check_kernel)."""
+    off (knob pll_pipe=0: the two-wave runner, checked by pll_check_kernel).  mixed: the streams
+    at three trigOffsets (2^22 / 2^21 / 2^20 + k, as a set_state or seek can leave them), so the
+    host's bounds differ and the segment runners (two-wave, saturated, lane) take them, checked."""
     ns, nb, bb = 300, 24, 12800
     ins = np.stack([iqgen.make("synth:%d" % (900 + s % 7), (nb + 2) * bb) for s in range(ns)])
     outs = []
     for pipe in ("1", "0"):
-        monkeypatch.setenv("FMRX_PLL_PIPE", pipe)
+        knobs(monkeypatch, fmrx, pll_pipe=float(pipe))
         with fmrx.Receiver(0, fmrx.STEREO, n_streams=ns) as rx:
             rx.process(ins[:, : 2 * bb])
             blob = bytearray(rx.get_state())
             hdr = np.frombuffer(bytes(blob[:40]), np.uint32)
             pll_off = 40 + ns * (int(hdr[6]) + 4 * int(hdr[7]) + 4 * 64)
             pll = np.frombuffer(bytes(blob[pll_off: pll_off + ns * 32]), np.float32).reshape(ns, 8).copy()
-            pll[:, 5] = 4194304.0 - 6000.0
+            if mixed:
+                pll[:, 5] = np.array([(4194304.0, 2097152.0, 1048576.0)[k % 3] + k for k in range(ns)], np.float32)
+            else:
+                pll[:, 5] = 4194304.0 - 6000.0
             blob[pll_off: pll_off + ns * 32] = pll.tobytes()
             rx.set_state(bytes(blob))
             counts = torch.zeros(2, dtype=torch.int64, device="cuda")
@@ -997,13 +1007,13 @@ def test_pipe_runner_streams(fmrx, monkeypatch):
 
 
 def test_predicted_runner_rows(fmrx, monkeypatch):
-    """pll_pred.hip with two streams a wave (1,100 streams: 16-lane rows; FMRX_PLL_PRED=2 launches
+    """pll_pred.hip with two streams a wave (1,100 streams: 16-lane rows; knob pll_pred=2 launches
     it although its 550 two-wave groups would share SIMDs, where the host leaves such counts to
     the lane runner), every stream put at its own trigOffset in [2^21, 2^21 + 1100) through the
     state blob -- except stream 5, at 1,000, which sends its wave (streams 4 and 5) to the lane
     runner -- 40 blocks in one call, every batch verified, and streams on both sides compared
     with the same stream alone."""
-    monkeypatch.setenv("FMRX_PLL_PRED", "2")
+    knobs(monkeypatch, fmrx, pll_pred=2)
     ns, nb, bb = 1100, 40, 12800
     ins = np.stack([iqgen.make("synth:%d" % (700 + s % 5), (nb + 2) * bb) for s in range(ns)])
     with fmrx.Receiver(0, fmrx.STEREO, n_streams=ns) as rx:
@@ -1209,12 +1219,11 @@ def test_rds_call_split_and_reset(fmrx, orc):
         assert same(rx.rds_block(demod)["rds"], z["rds"])
 
 
-@pytest.mark.parametrize("env", [{"FMRX_PLL_SPEC": "0"}, {"FMRX_PLL_SPEC_INJECT": "3"}])
+@pytest.mark.parametrize("env", [{"pll_spec": "0"}, {"pll_inject": "3"}])
 def test_rds_pll_speculation_fallbacks(fmrx, monkeypatch, env):
     """The RDS loop (114 kHz, ncoScale 0.5) through the same speculative launch: the plain
     certified launch and a runner with one corrupted batch both give the fixture's bits."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    knobs(monkeypatch, fmrx, **{k: float(v) for k, v in env.items()})
     z = load_rds("m0_rds57")
     with fmrx.Receiver(0, fmrx.MONO) as rx:
         assert same(rx.rds_block(z["demod"])["rds"], z["rds"])

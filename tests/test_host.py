@@ -136,3 +136,24 @@ def test_product_and_tools_do_not_use_oracle():
     pat = re.compile(r"import oracle|from oracle|[\"']oracle[\"']|oracle/_ref|_ref/project")
     bad = [f for f in files if os.path.isfile(f) and pat.search(open(f, errors="replace").read())]
     assert files and not bad, bad
+
+
+def test_product_library_reads_no_output_changing_hook(fmrx):
+    """The product libfmrx.so (Makefile `all`) names no environment hook that changes what the
+    kernels compute or that forces the PLL runners off their normal path: the stage-removal
+    ablation (FMRX_ABLATE) is compiled only into the A/B build, and the PLL test hooks (batch
+    corruption, forced misses, skewed trigOffset bounds) exist only as per-context knobs
+    (fmrx_debug_set_knob) that the tests set.  The remaining variables are tuning switches read once
+    at context creation (the same bits either way)."""
+    import re
+
+    path = os.path.join(REPO, "software-defined-radio-course-project_amd", "libfmrx.so")
+    data = open(path, "rb").read()
+    names = set(re.findall(rb"FMRX_[A-Z0-9_]+", data))
+    hooks = {b"FMRX_ABLATE", b"FMRX_PLL_SPEC_INJECT", b"FMRX_PLL_HINT_SKEW", b"FMRX_PLL_PIPE_MISS"}
+    assert not names & hooks, names & hooks
+    tuning = {b"FMRX_PLL_SPEC", b"FMRX_PLL_SAT", b"FMRX_PLL_PRED", b"FMRX_PLL_PIPE", b"FMRX_PLL_IDX",
+              b"FMRX_STEREO_CHUNKS", b"FMRX_MONO_SPLIT", b"FMRX_BPF_TILE", b"FMRX_HALO_KERNEL", b"FMRX_MONO_VARIANT",
+              b"FMRX_PLL_CNT"}
+    assert names <= tuning, names - tuning
+    assert set(fmrx.KNOBS) >= {"pll_inject", "pll_pipe_miss", "pll_hint_skew"}

@@ -4,7 +4,7 @@ resampler over a 7,497-tap prototype, 51 taps per output) on 1 GiB of device-res
 synthetic I/Q per mode.  One step = fmrx_process_device over the whole GiB (RF front end +
 demod + audio resampler + S16).  Prints one JSON line per mode.
 
-    python tools/bench_modes.py [--modes 0 1 2 3] [--steps 5] [--rf-taps 51]
+    python tools/bench_modes.py [--modes 0 1 2 3] [--steps 5] [--rf-taps 51] [--warmup-seconds 1]
 """
 import argparse
 import json
@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--modes", type=int, nargs="+", default=[0, 1, 2, 3])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--rf-taps", type=int, default=51)
+    ap.add_argument("--warmup-seconds", type=float, default=1.0,
+                    help="untimed back-to-back steps first (the clock ramp, DESIGN §5.1), as bench.py")
     args = ap.parse_args()
     import torch
 
@@ -37,6 +39,11 @@ def main():
             rx.synth_device(100 + mode, 0, nb * bb // 2, d_iq.data_ptr())
             rx.process_device(d_iq.data_ptr(), nb, d_pcm.data_ptr())  # warm-up
             rx.synchronize()
+            t_w = time.perf_counter()
+            while time.perf_counter() - t_w < args.warmup_seconds:
+                for _ in range(64):
+                    rx.process_device(d_iq.data_ptr(), nb, d_pcm.data_ptr())
+                rx.synchronize()
             rx.kernel_timing(reset=1)
             t0 = time.perf_counter()
             for _ in range(args.steps):

@@ -13,9 +13,9 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 120 python tools/mono_stamps.py > $OUT/mono_stamps.json 2> $OUT/mono_stamps.err || exit 1
 for a in $LIST; do
-  FMRX_ABLATE=$a timeout -k 10 120 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-other-configs \
+  FMRX_LIB_PATH=software-defined-radio-course-project_amd/build_ab/libfmrx.so FMRX_ABLATE=$a timeout -k 10 120 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-other-configs \
       > $OUT/bench_$a.json 2> $OUT/bench_$a.err || exit 2
-  FMRX_ABLATE=$a timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY \
+  FMRX_LIB_PATH=software-defined-radio-course-project_amd/build_ab/libfmrx.so FMRX_ABLATE=$a timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY \
       SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -T -d $OUT/pmc_$a -o run \
       --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-other-configs \
       > $OUT/pmc_$a.log 2>&1 || exit 3

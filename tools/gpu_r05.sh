@@ -1,0 +1,52 @@
+#!/bin/bash
+# tools/gpu_r05.sh <tag> [steps...] — round-5 GPU steps, each under its own time limit, stopping at
+# the first failure.  Steps:
+#   cnt       tools/ubench_cnt (chain forms' dependent latency per piece)
+#   mode2     configs[3] (mode-2 mono, 1 GiB) profile of record: a warm (>= 1.5 s) kernel trace and
+#             separate PMC passes FETCH_SIZE / WRITE_SIZE / GRBM (tools/bench_modes.py --modes 2)
+#   tests     the whole GPU suite
+#   pll       the PLL / stereo GPU tests
+#   stages    tools/stage_times.py (one 10 s stream, configs[4], configs[2] stage times)
+#   bench     bench.py without the CPU baseline
+#   pllcnt    the PLL / stereo GPU tests with the count runner on the forms in $CNT (bitmask, default 31)
+#   envab     stage_times per value of $ENVVAR in $VALS ($STARGS: its arguments), alternating, twice
+#   smoke     __graft_entry__.smoke()
+set -o pipefail
+TAG=${1:-r05}; shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+M2="python3 tools/bench_modes.py --modes 2 --steps 20 --warmup-seconds 1.5"
+for step in "$@"; do
+  case $step in
+    cnt) timeout -k 10 120 tools/ubench_cnt > $OUT/ubench_cnt.txt 2>&1 || { tail $OUT/ubench_cnt.txt; exit 7; }
+         cat $OUT/ubench_cnt.txt ;;
+    mode2) timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/m2_kt -o run --output-format csv -- \
+             $M2 > $OUT/m2_kt.log 2>&1 || { tail $OUT/m2_kt.log; exit 8; }
+           timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/m2_fetch -o run --output-format csv -- \
+             $M2 > $OUT/m2_fetch.log 2>&1 || { tail $OUT/m2_fetch.log; exit 8; }
+           timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/m2_write -o run --output-format csv -- \
+             $M2 > $OUT/m2_write.log 2>&1 || { tail $OUT/m2_write.log; exit 8; }
+           timeout -k 10 240 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT -d $OUT/m2_grbm -o run --output-format csv -- \
+             $M2 > $OUT/m2_grbm.log 2>&1 || { tail $OUT/m2_grbm.log; exit 8; }
+           cat $OUT/m2_kt.log ;;
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
+           tail -2 $OUT/tests.log ;;
+    pll) timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "pll or stereo or bench_config or trig_hint or refdata or cli or index" > $OUT/pll.log 2>&1 || { tail -40 $OUT/pll.log; exit 2; }
+         tail -2 $OUT/pll.log ;;
+    stages) timeout -k 10 300 python tools/stage_times.py > $OUT/stages.json 2> $OUT/stages.err || { tail $OUT/stages.err; exit 3; }
+            cat $OUT/stages.json ;;
+    bench) timeout -k 10 400 python bench.py --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err || { tail $OUT/bench.err; exit 4; }
+           python -c "import json; j=json.load(open('$OUT/bench.json')); print(j['value'], j['roofline']['kernel_ms'], json.dumps(j.get('baseline_configs',{}))[:1500])" ;;
+    pllcnt) FMRX_PLL_CNT=${CNT:-31} timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "pll or stereo or index or bench_config or refdata or cli or pipe" > $OUT/pllcnt.log 2>&1 || { tail -40 $OUT/pllcnt.log; exit 12; }
+         tail -2 $OUT/pllcnt.log ;;
+    envab) # stage_times (configs[4], one 10 s stream, configs[2]) per value of $ENVVAR in $VALS, alternating, twice
+         for r in 1 2; do for v in $VALS; do
+           env $ENVVAR=$v timeout -k 10 300 python tools/stage_times.py $STARGS > $OUT/envab_${r}_$v.json 2>> $OUT/envab.err || { tail $OUT/envab.err; exit 18; }
+           echo "$r $ENVVAR=$v $(python tools/stage_summary.py $OUT/envab_${r}_$v.json)"
+         done; done ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail $OUT/smoke.log; exit 5; }
+           tail -1 $OUT/smoke.log ;;
+  esac
+done
+echo all done
