@@ -151,6 +151,8 @@ def main() -> None:
                          "stereo configs[4] at every N)")
     ap.add_argument("--streams-seconds", type=float, default=60.0,
                     help="configs[4] stream length (256 stereo streams sharded over the ranks)")
+    ap.add_argument("--gather-chunks", type=int, default=4,
+                    help="configs[4] at N > 1: time chunks whose PCM is gathered beside the next one's processing")
     args = ap.parse_args()
 
     import numpy as np
@@ -305,7 +307,7 @@ def main() -> None:
         rx.close()
         torch.cuda.empty_cache()
         line["baseline_configs"] = other_configs(fmrx) if world == 1 else {}
-        c4 = streams_config(fmrx, world, rank, dev if world > 1 else 0, args.streams_seconds)
+        c4 = streams_config(fmrx, world, rank, dev if world > 1 else 0, args.streams_seconds, args.gather_chunks)
         if rank == 0:
             line["baseline_configs"]["configs[4]"] = c4
     if rank == 0:
@@ -540,7 +542,7 @@ def parity_vs_reference(key: str, d_iq, d_pcm, keep: bool = False):
     return (res, h_iq, h_pcm) if keep else res
 
 
-def streams_config(fmrx, world: int, rank: int, dev: int, seconds: float) -> dict | None:
+def streams_config(fmrx, world: int, rank: int, dev: int, seconds: float, gather_chunks: int = 1) -> dict | None:
     """BASELINE configs[4] at this N (extra key; `value` stays configs[1]): 256 independent
     mode-0 stereo streams of `seconds` each, sharded contiguously over the ranks (one process per
     GPU), each rank's shard one device-resident multi-stream call, the S16 PCM gathered to rank 0
@@ -555,7 +557,8 @@ def streams_config(fmrx, world: int, rank: int, dev: int, seconds: float) -> dic
     geo = fmrx.geometry(fmrx.default_config(0, fmrx.STEREO))
     expect = iqgen.stream_hashes(256, int(seconds * geo.rf_fs * 2 // geo.block_bytes)) or None
     try:  # streams_leg agrees on failure across ranks before each collective (dist.run_leg)
-        res = dmod.streams_leg(fmrx, 256, seconds, world, rank, dev, expect=expect, profile=stage_latency)
+        res = dmod.streams_leg(fmrx, 256, seconds, world, rank, dev, expect=expect, profile=stage_latency,
+                               gather_chunks=gather_chunks)
     except Exception as e:  # the headline line must still print
         res = {"error": repr(e)} if rank == 0 else None
     torch.cuda.empty_cache()

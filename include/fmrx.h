@@ -255,7 +255,7 @@ int fmrx_debug_stage_timing(fmrx_ctx* ctx, int op, double* ms, double* steps, lo
 #define FMRX_KNOB_PLL_INJECT 9        /* test hook: runners corrupt batch 1+(k+s)%(nb-1) of stream s  */
 #define FMRX_KNOB_PLL_PIPE_MISS 10    /* test hook: self-certifying runners miss interval k            */
 #define FMRX_KNOB_PLL_HINT_SKEW 11    /* test hook: host trigOffset bounds shifted by value samples    */
-#define FMRX_KNOB_PLL_CNT 12          /* bit f-17: count runner for form f's range        FMRX_PLL_CNT  */
+#define FMRX_KNOB_PLL_CNT 12          /* bit f-17: count runner for form f's range (12)   FMRX_PLL_CNT  */
 int fmrx_debug_set_knob(fmrx_ctx* ctx, int knob, double value);
 
 #ifdef __cplusplus

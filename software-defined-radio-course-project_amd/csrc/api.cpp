@@ -750,7 +750,7 @@ static fmrx_ctx::Knobs knobs_from_env() {
     k.pll.pred = get("FMRX_PLL_PRED", 1);
     k.pll.pipe = get("FMRX_PLL_PIPE", 1);
     k.pll.idx = get("FMRX_PLL_IDX", 2);
-    k.pll.cnt = get("FMRX_PLL_CNT", 0);
+    k.pll.cnt = get("FMRX_PLL_CNT", kPllCntDefault);
     k.stereo_chunks = std::max(0, get("FMRX_STEREO_CHUNKS", 0));
     k.mono_split = get("FMRX_MONO_SPLIT", -1);
     k.bpf_tile = get("FMRX_BPF_TILE", 1);

@@ -109,7 +109,7 @@ struct PllKnobs {
     int pred = 1;        // 0: no predicted runners; 2: the two-wave one even where waves share SIMDs
     int pipe = 1;        // 0: no three-wave runner (FMRX_PLL_PIPE)
     int idx = 2;         // index runner from 2^17 (2), from 2^18 (1), off (0) (FMRX_PLL_IDX)
-    int cnt = 0;         // bit f - 17: the count runner takes form f's range (FMRX_PLL_CNT)
+    int cnt = 12;        // bit f - 17: the count runner takes form f's range (FMRX_PLL_CNT; kPllCntDefault)
     int inject = -1;     // test hook: the runners corrupt batch 1 + (k + s) % (nb - 1) of stream s
     int pipe_miss = -1;  // test hook: the self-certifying runners report interval k as missed
     double skew = 0.0;   // test hook: the host's trigOffset bounds shifted by this many samples
@@ -172,6 +172,12 @@ int launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t 
 int launch_pll_cnt(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
                    float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats,
                    unsigned* redos = nullptr);
+// The count runner's forms by default: [2^19, 2^20) and [2^20, 2^21) (bits 2, 3).  Same-box A/B,
+// two alternating rounds (profiles/r05/ab_cnt12/): one 10 s stream 0.1093 -> 0.0923 s, configs[4]
+// 0.430 -> 0.418 s, configs[2] 1.240 -> 1.222 s.  [2^17, 2^19) stay on the index runner (the
+// count form's 31-candidate evaluators bound it: 68-73 ns a step against 55), [2^21, 2^22) on the
+// three-wave runner (profiles/r05/rprof/).
+constexpr int kPllCntDefault = 12;
 // fmrx_debug_pll_redos: per stream, intervals the self-certifying runners redid, by form (0 index,
 // 1 three-wave 16-step, 2 three-wave 64-step five candidates, 3 three candidates)
 constexpr int kPllRedoForms = 4;

@@ -1391,11 +1391,14 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
     constexpr int CH = NI < 16 ? NI : 16;          // the chain's steps a burst of reads
     static_assert(NC % 2 == 1 && NP <= 64, "an odd window within a wave");
     static_assert(NI == 16 || NI == 32 || NI == 64, "a row of counts in a VGPR");
-    // rings of four intervals (interval k in slot k & 3): the T and E rows of each step, bits(c_base)
-    // - 1 of each step (the trigArg store), the chain's count of each step, its (integ, phase) at
-    // the interval's end, "redone exactly"
-    __shared__ float sT[4][NI][NP];
-    __shared__ float sE[4][NI][NP];
+    // rings of four intervals (interval k in slot k & 3): the T and E rows of each pair of steps
+    // interleaved by row slot (sR[.][p][l] = T_2p(l), E_2p(l), T_2p+1(l), E_2p+1(l): one 16-byte
+    // read a lane gives the chain two steps' rows), bits(c_base) - 1 of each step (the trigArg
+    // store), the chain's count of each step, its (integ, phase) at the interval's end, "redone
+    // exactly"
+    __shared__ float4 sR[4][NI / 2][NP];
+    auto sT = [&](int sl, int J, int l) -> float& { return reinterpret_cast<float*>(&sR[sl][J >> 1][l])[2 * (J & 1)]; };
+    auto sE = [&](int sl, int J, int l) -> float& { return reinterpret_cast<float*>(&sR[sl][J >> 1][l])[2 * (J & 1) + 1]; };
     __shared__ uint32_t sbase[4][NI];
     __shared__ int srow[4][NI];
     __shared__ float2 sst[4];
@@ -1433,9 +1436,9 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
             exact(p, c, 0, n);
             if (t == 0) {
                 S[0] = p.integ; S[1] = p.phase; S[2] = p.fbI; S[3] = p.fbQ; S[5] = p.trig;
-                if (stats) {
-                    if (!in_domain) atomicAdd(stats, (unsigned long long)nb);
-                    atomicAdd(stats + 1, (unsigned long long)nb);
+                if (stats) {  // in 16-step batches, as every runner counts
+                    if (!in_domain) atomicAdd(stats, (unsigned long long)(n / kPllBatch));
+                    atomicAdd(stats + 1, (unsigned long long)(n / kPllBatch));
                 }
             }
         }
@@ -1444,9 +1447,9 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
     auto j0 = [](int k) { return NI * k; };  // interval k's first step
     // the rows' constant slots, once: T slot NC + 1 = +inf (never counted), E slots 0 and NC + 1 NaN
     for (int q = threadIdx.x; q < 4 * NI; q += 64 * (1 + NW)) {
-        sT[q / NI][q % NI][NC + 1] = __builtin_inff();
-        sE[q / NI][q % NI][0] = __builtin_nanf("");
-        sE[q / NI][q % NI][NC + 1] = __builtin_nanf("");
+        sT(q / NI, q % NI, NC + 1) = __builtin_inff();
+        sE(q / NI, q % NI, 0) = __builtin_nanf("");
+        sE(q / NI, q % NI, NC + 1) = __builtin_nanf("");
     }
 
     if (w > 0) {
@@ -1475,7 +1478,7 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
                                             pll_iv(v[u]), ok);
                 // a window that is not of positive finite floats never certifies: c0 < 2^126
                 const bool fin = cb > (uint32_t)HC && cb < 0x7F000000u;
-                sE[sl][J][kc + 1] = ok && fin ? e : __builtin_nanf("");
+                sE(sl, J, kc + 1) = ok && fin ? e : __builtin_nanf("");
             }
 #pragma unroll
             for (int u = 0; u < NT; u++) {
@@ -1484,7 +1487,7 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
                 const int J = q / (NC + 1), kc = q % (NC + 1);
                 const double pr = pr_at(j0(k) + J);
                 const uint32_t cb = __builtin_bit_cast(uint32_t, (float)(pr + (double)phase_ref));
-                sT[sl][J][kc] = phase_thr_exact(pr, cb - (uint32_t)HC + (uint32_t)kc);
+                sT(sl, J, kc) = phase_thr_exact(pr, cb - (uint32_t)HC + (uint32_t)kc);
                 if (kc == 0) sbase[sl][J] = cb - (uint32_t)HC - 1u;
             }
         };
@@ -1567,9 +1570,12 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
                 // the burst's rows before its steps
                 float T[CH], E[CH];
 #pragma unroll
-                for (int J = 0; J < CH; J++) {
-                    T[J] = sT[is][H * CH + J][ls];
-                    E[J] = sE[is][H * CH + J][ls];
+                for (int J = 0; J < CH; J += 2) {
+                    const float4 r = sR[is][(H * CH + J) / 2][ls];
+                    T[J] = r.x;
+                    E[J] = r.y;
+                    T[J + 1] = r.z;
+                    E[J + 1] = r.w;
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 unroll_ic(
@@ -1636,9 +1642,9 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
     exact(q, c, jf, n);
     if (t == 0) {
         S[0] = q.integ; S[1] = q.phase; S[2] = q.fbI; S[3] = q.fbQ; S[5] = q.trig;
-        if (stats) {
-            atomicAdd(stats, n_inj);  // "resumed": the inject hook's forced redos only
-            atomicAdd(stats + 1, (unsigned long long)nb);
+        if (stats) {  // in 16-step batches, as every runner counts
+            atomicAdd(stats, n_inj * (NI / kPllBatch));  // "resumed": the inject hook's forced redos only
+            atomicAdd(stats + 1, (unsigned long long)(n / kPllBatch));
         }
         if (redos) atomicAdd(&redos[kPllRedoForms * (size_t)s + (lo < kPllPipeMinLow ? 0 : lo < kPllPipeMin5 ? 1 : lo < kPllPipeMin ? 2 : 3)],
                              (unsigned)n_redo);
@@ -1813,8 +1819,8 @@ int launch_pll_cnt(hipStream_t s, const float* io, int n, int n_streams, size_t 
         case 20:
             return cnt_launch<64, 15, 4>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
                                          kPllPipeMinLow, kPllPipeMin5 - 1.0f, stats, redos);
-        default:
-            return cnt_launch<64, 7, 4>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
+        default:  // three waves a stream, as the three-wave runner it would replace
+            return cnt_launch<64, 7, 2>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
                                         kPllPipeMin5, kPllPipeMin - 1.0f, stats, redos);
     }
 }

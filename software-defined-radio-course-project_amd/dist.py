@@ -111,6 +111,35 @@ def per_rank(values: Sequence[float], pg: bool, device=None) -> list[list[float]
     return [p.tolist() for p in parts]
 
 
+def gather_chunked(chunks, n_streams: int, pcm_len: int, world: int, rank: int, pg: bool):
+    """Gather a rank's PCM time chunk by time chunk as each one finishes: `chunks` is a list of
+    (col0, tensor[n_local, cols], done) with `done` a torch.cuda.Event recorded after the chunk's
+    work on the stream that computes it (None: already complete).  RCCL: the collective's stream
+    waits for the event, so chunk c's gather runs beside chunk c + 1's processing; gloo: the host
+    waits for chunk c alone, then moves it.  Returns (rank 0: [n_streams, pcm_len], else None;
+    the time the last chunk's processing was seen complete)."""
+    import time
+
+    nccl = pg and dist.get_backend() == "nccl"
+    full = None
+    t_proc = None
+    for k, (c0, part, done) in enumerate(chunks):
+        last = k == len(chunks) - 1
+        if done is not None:
+            if nccl and not last:
+                torch.cuda.current_stream(part.device).wait_event(done)
+            else:
+                done.synchronize()
+        if last:
+            t_proc = time.perf_counter()
+        got = gather_pcm(part, n_streams, part.shape[1], world, rank) if pg else part
+        if got is not None:
+            if full is None:
+                full = torch.empty((n_streams, pcm_len), dtype=got.dtype, device=got.device)
+            full[:, c0:c0 + got.shape[1]] = got
+    return full, t_proc
+
+
 def run_leg(setup: Callable[[], object], process: Callable[[object], torch.Tensor], n_streams: int, pcm_len: int,
             world: int, rank: int, pg: bool, device=None, cleanup: Callable[[object], None] | None = None,
             post: Callable[[object], dict] | None = None) -> dict:
@@ -141,17 +170,22 @@ def run_leg(setup: Callable[[], object], process: Callable[[object], torch.Tenso
         local = None
         try:
             local = process(state)
-            assert local.shape[1:] == (pcm_len,), (tuple(local.shape), pcm_len)
+            if isinstance(local, torch.Tensor):
+                assert local.shape[1:] == (pcm_len,), (tuple(local.shape), pcm_len)
         except Exception as e:  # noqa: BLE001
             err = f"rank {rank} process: {e!r}"
         t1 = time.perf_counter()
         if not all_ok(err is None, pg, device):
             return {"error": err or "another rank failed in the timed step; gather skipped"}
-        gathered = gather_pcm(local, n_streams, pcm_len, world, rank) if pg else local
+        if isinstance(local, torch.Tensor):
+            gathered = gather_pcm(local, n_streams, pcm_len, world, rank) if pg else local
+            t_proc = t1
+        else:  # time chunks enqueued: each gathered as soon as it is done, beside the later ones
+            gathered, t_proc = gather_chunked(local, n_streams, pcm_len, world, rank, pg)
         if device is not None and torch.cuda.is_available():
             torch.cuda.synchronize(device)
         t2 = time.perf_counter()
-        ranks = per_rank([t2 - t0, t1 - t0, t2 - t1], pg, device)
+        ranks = per_rank([t2 - t0, t_proc - t0, t2 - t_proc], pg, device)
         res = {"per_rank": ranks, "total": max(r[0] for r in ranks), "process": max(r[1] for r in ranks),
                "gather": max(r[2] for r in ranks)}
         if rank == 0:
@@ -169,7 +203,8 @@ def run_leg(setup: Callable[[], object], process: Callable[[object], torch.Tenso
 
 def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, device: int,
                 mode: int = 0, expect: dict | None = None, warmup: bool = True,
-                collective: bool | None = None, profile: Callable | None = None) -> dict | None:
+                collective: bool | None = None, profile: Callable | None = None,
+                gather_chunks: int = 1) -> dict | None:
     """BASELINE configs[4] as one timed step: `n_streams` independent stereo streams (stream id
     = synth seed) of `seconds` each, this rank's contiguous shard processed as ONE multi-stream
     device-resident call, then the S16 PCM gathered to rank 0 (RCCL over xGMI; gloo rehearses
@@ -182,8 +217,11 @@ def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, dev
     PCM (`parity` says "unpinned" when none are recorded for this length).  `collective`
     (default: world > 1) routes the barrier, gather and timing reduction through the process
     group; without it (one rank, no process group) the rank's PCM is the result.  A failure on
-    any rank is agreed on before each collective (run_leg), so no rank hangs in one.  Returns
-    rank 0's result dict (None elsewhere)."""
+    any rank is agreed on before each collective (run_leg), so no rank hangs in one.
+    `gather_chunks` K > 1 (with a process group): the shard runs as K calls over consecutive time
+    chunks (the context carries every state across them: the same PCM as one call), each chunk's
+    PCM gathered as soon as it is done while the next is processed (gather_chunked), so only the
+    last chunk's gather follows the processing.  Returns rank 0's result dict (None elsewhere)."""
     import hashlib
     import time
 
@@ -194,26 +232,34 @@ def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, dev
     bb = geo.block_bytes
     nb = int(seconds * geo.rf_fs * 2 // bb)
     pcm_len = nb * geo.pcm_samples
+    K = max(1, min(gather_chunks, nb)) if pg else 1
+    cuts = [nb * k // K for k in range(K + 1)]  # block boundaries of the time chunks
     t_synth = [0.0]
     redos = [None]  # this rank's streams x 4 redone intervals (fmrx_debug_pll_redos), warm-up call
 
     def setup():
         rx = fmrx.Receiver(mode, fmrx.STEREO, n_streams=max(1, len(ids)), device=device)
         try:
-            iq = torch.empty((max(1, len(ids)), nb * bb), dtype=torch.uint8, device=dev)
-            out = torch.empty((len(ids), pcm_len), dtype=torch.int16, device=dev)
+            # one input and one output buffer a time chunk (stream-major within the chunk)
+            iqs = [torch.empty((max(1, len(ids)), (cuts[k + 1] - cuts[k]) * bb), dtype=torch.uint8, device=dev)
+                   for k in range(K)]
+            outs = [torch.empty((len(ids), (cuts[k + 1] - cuts[k]) * geo.pcm_samples), dtype=torch.int16,
+                                device=dev) for k in range(K)]
             torch.cuda.synchronize(dev)
             t = time.perf_counter()
             if ids:
-                rx.synth_device_streams(ids, 0, nb * bb // 2, iq.data_ptr(), nb * bb)
+                for k in range(K):
+                    rx.synth_device_streams(ids, cuts[k] * bb // 2, (cuts[k + 1] - cuts[k]) * bb // 2,
+                                            iqs[k].data_ptr(), (cuts[k + 1] - cuts[k]) * bb)
                 rx.synchronize()
             t_synth[0] = time.perf_counter() - t
             if ids and warmup:
-                # the untimed warm-up call does the timed call's work exactly (same input, same
+                # the untimed warm-up does the timed step's work exactly (same input, same
                 # power-on state): the runners' per-stream redo counts are taken here
                 redo = torch.zeros((len(ids), 4), dtype=torch.int32, device=dev)
                 rx.debug_pll_redos(redo.data_ptr())
-                rx.process_device(iq.data_ptr(), nb, out.data_ptr())
+                for k in range(K):
+                    rx.process_device(iqs[k].data_ptr(), cuts[k + 1] - cuts[k], outs[k].data_ptr())
                 rx.synchronize()
                 rx.debug_pll_redos(None)
                 redos[0] = redo.cpu().numpy()
@@ -221,20 +267,35 @@ def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, dev
         except Exception:
             rx.close()
             raise
-        return rx, iq, out
+        return rx, iqs, outs
 
     def process(state):
-        rx, iq, out = state
-        if ids:
-            rx.process_device(iq.data_ptr(), nb, out.data_ptr())
-            rx.synchronize()
-        return out
+        rx, iqs, outs = state
+        if K == 1:
+            if ids:
+                rx.process_device(iqs[0].data_ptr(), nb, outs[0].data_ptr())
+                rx.synchronize()
+            return outs[0]
+        ext = torch.cuda.ExternalStream(rx.stream(), device=dev)
+        chunks = []
+        for k in range(K):
+            done = None
+            if ids:
+                rx.process_device(iqs[k].data_ptr(), cuts[k + 1] - cuts[k], outs[k].data_ptr())
+                done = torch.cuda.Event()
+                done.record(ext)
+            chunks.append((cuts[k] * geo.pcm_samples, outs[k], done))
+        return chunks
 
     # profile(rx, run) (optional, rank 0): one more call of rank 0's shard, e.g. with the stage
     # timing armed (bench.stage_latency); its result is the line's `latency`
     post = None
     if profile is not None and ids:
-        post = lambda st: profile(st[0], lambda: st[0].process_device(st[1].data_ptr(), nb, st[2].data_ptr()))
+        def post(st):
+            def run():
+                for k in range(K):
+                    st[0].process_device(st[1][k].data_ptr(), cuts[k + 1] - cuts[k], st[2][k].data_ptr())
+            return profile(st[0], run)
     res = run_leg(setup, process, n_streams, pcm_len, world, rank, pg, dev, cleanup=lambda st: st[0].close(),
                   post=post)
     if rank != 0:
@@ -245,11 +306,18 @@ def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, dev
     assert gathered.shape == (n_streams, pcm_len), gathered.shape
     sig_s = nb * bb / 2 / geo.rf_fs
     total = res["total"]
+    max_local = len(shard(n_streams, world, 0))
     out = {"workload": f"BASELINE configs[4]: {n_streams} independent mode-{mode} stereo streams x {sig_s:g} s, "
                        f"{world} rank(s), streams sharded contiguously"
-                       + (", S16 PCM gathered to rank 0" if pg else ", PCM left on the one rank (no gather)"),
+                       + (", S16 PCM gathered to rank 0" if pg else ", PCM left on the one rank (no gather)")
+                       + (f" in {K} time chunks, each gathered beside the next one's processing" if K > 1 else ""),
            "n_gpus": world, "seconds": round(total, 4), "seconds_process": round(res["process"], 4),
            "seconds_gather": round(res["gather"], 4), "gather_bytes": int(gathered.numel() * 2),
+           "gather_chunks": K,
+           # every rank sends an equal (padded) message per chunk; rank 0 receives world of them
+           "gather_bytes_sent_per_rank": int(max_local * pcm_len * 2) if pg else 0,
+           "gather_GBs_after_processing": (round(max_local * pcm_len * 2 * world / K / res["gather"] / 1e9, 2)
+                                           if pg and res["gather"] > 0 else None),
            "MS_per_s": round(n_streams * nb * bb / 2 / total / 1e6, 1),
            "stream_seconds_per_s": round(n_streams * sig_s / total, 1),
            "x_realtime_per_stream": round(sig_s / total, 2), "synth_seconds_untimed": round(t_synth[0], 3),

@@ -63,13 +63,26 @@ def leg_with_failure(d, n_streams, world, rank, where):
     return d.run_leg(setup, run, n_streams, NB * NA * 2, world, rank, True)
 
 
+def leg_chunked(d, n_streams, world, rank, n_chunks=3):
+    """dist.run_leg with the PCM handed over as time chunks (dist.gather_chunked: each chunk
+    gathered on its own, rank 0 stitching the columns back)."""
+    def run(ids):
+        full = process(ids)
+        cols = full.shape[1]
+        cuts = [cols * k // n_chunks for k in range(n_chunks + 1)]
+        return [(cuts[k], full[:, cuts[k]:cuts[k + 1]].contiguous(), None) for k in range(n_chunks)]
+
+    return d.run_leg(lambda: list(d.shard(n_streams, world, rank)), run, n_streams, NB * NA * 2, world, rank, True)
+
+
 def main():
     n_streams, out_path = int(sys.argv[1]), sys.argv[2]
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     d = iqgen.load_module("dist")
-    if len(sys.argv) > 3 and sys.argv[3] in ("setup", "process", "ok"):  # dist.run_leg failure agreement
-        res = leg_with_failure(d, n_streams, world, rank, sys.argv[3])
+    if len(sys.argv) > 3 and sys.argv[3] in ("setup", "process", "ok", "chunks"):  # dist.run_leg
+        res = (leg_chunked(d, n_streams, world, rank) if sys.argv[3] == "chunks"
+               else leg_with_failure(d, n_streams, world, rank, sys.argv[3]))
         if rank == 0:
             if "error" in res:
                 np.save(out_path, np.frombuffer(res["error"].encode(), np.uint8))

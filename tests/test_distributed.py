@@ -80,3 +80,11 @@ def test_run_leg_world2_gathers(orc, tmp_path):
     got = _run_world2(tmp_path, 3, "ok")
     want = np.stack([orc.run(MODE, 51, iqgen.make(f"rand:{100 + i}", NB * BB), ["pcm"])["pcm"] for i in range(3)])
     assert np.array_equal(got, want)
+
+
+def test_run_leg_world2_gathers_time_chunks(orc, tmp_path):
+    """The chunked gather (dist.gather_chunked, bench.py's configs[4] at N > 1): each rank hands
+    over its PCM as three time chunks, gathered one by one; rank 0 stitches the same PCM."""
+    got = _run_world2(tmp_path, 3, "chunks")
+    want = np.stack([orc.run(MODE, 51, iqgen.make(f"rand:{100 + i}", NB * BB), ["pcm"])["pcm"] for i in range(3)])
+    assert np.array_equal(got, want)

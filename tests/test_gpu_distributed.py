@@ -41,9 +41,9 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _gpu_world(tmp_path, world, *args):
+def _gpu_world(tmp_path, world, *args, out_name="pcm.npy"):
     port = _free_port()
-    out = tmp_path / "pcm.npy"
+    out = tmp_path / out_name
     procs = []
     for r in range(world):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
@@ -57,12 +57,12 @@ def _gpu_world(tmp_path, world, *args):
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    return np.load(out)
+    return out
 
 
 @pytest.mark.parametrize("n_streams,n_blocks,check", [(256, 4, (0, 127, 128, 255)), (5, 3, (0, 2, 3, 4))])
 def test_configs4_sharded_stereo_world2_gloo(fmrx, orc, tmp_path, n_streams, n_blocks, check):
-    got = _gpu_world(tmp_path, 2, n_streams, n_blocks, 0, fmrx.STEREO)
+    got = np.load(_gpu_world(tmp_path, 2, n_streams, n_blocks, 0, fmrx.STEREO))
     bb, na = 12800, 128
     assert got.shape == (n_streams, n_blocks * na * 2)
     for sid in check:
@@ -87,3 +87,16 @@ def test_configs4_rccl_one_rank_bench_streams(fmrx):
     # the gathered PCM against the reference build's hashes (tests/golden/hashes.json
     # streams_c4_short), not against another GPU run
     assert res["checked_streams"] == [0, 7, 8, 15] and res["bit_exact_vs_reference"] is True
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_configs4_leg_world2_gloo_time_chunks(tmp_path, chunks):
+    """dist.streams_leg as bench.py runs configs[4] at N > 1, rehearsed with gloo on one device:
+    16 streams x 0.5 s in `chunks` time chunks, each chunk's PCM gathered as soon as its CUDA
+    event completes (dist.gather_chunked) while the next chunk is processed; the stitched PCM
+    equals the reference build's hashes (tests/golden/hashes.json streams_c4_short)."""
+    path = _gpu_world(tmp_path, 2, "leg", 16, 0.5, chunks, out_name="leg.json")
+    res = json.loads(path.read_text())
+    assert res["gather_chunks"] == chunks and res["n_gpus"] == 2, res
+    assert res["checked_streams"] == [0, 7, 8, 15] and res["bit_exact_vs_reference"] is True, res
+    assert res["gather_bytes_sent_per_rank"] == 8 * int(0.5 * 2400000 * 2 // 12800) * 256 * 2

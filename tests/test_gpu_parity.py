@@ -912,6 +912,44 @@ def test_pll_index_runner(fmrx, orc, monkeypatch, trig0, inject, idx):
         assert (resumed > 0) if inject is not None else (resumed == 0), (resumed, checked)
 
 
+@pytest.mark.parametrize("trig0", [131072.0, 262177.0, 524188.0, 700000.0, 1048500.0, 1048576.0, 1500000.0,
+                                   2097100.0, 3000000.0])
+@pytest.mark.parametrize("hook", [None, ("pll_inject", 5), ("pll_pipe_miss", 1), ("pll_pipe_miss", 300)])
+@pytest.mark.parametrize("cnt", [31, 0])
+def test_pll_count_runner(fmrx, orc, monkeypatch, trig0, hook, cnt):
+    """trigOffset in [2^17, 2^22) on the count runner (pll_pred.hip pll_cnt_kernel: one compare
+    of the phase against a row of exact thresholds and a bit count pick each step's e; knob
+    pll_cnt = 31: every form from 2^17 to 2^22 on it, 0: none -- the index and three-wave runners),
+    starting at each form's edge, just below the next edge (the call crosses into the next form)
+    and inside; with a forced miss (pll_inject: counted as resumed; pll_pipe_miss k: interval k
+    redone, k past the last: the last) the interval is redone exactly.  Bit-exact against the
+    oracle, state included."""
+    knobs(monkeypatch, fmrx, pll_cnt=cnt)
+    if hook is not None:
+        knobs(monkeypatch, fmrx, **{hook[0]: hook[1]})
+    n = 20000
+    rng = np.random.default_rng(int(trig0) % 991)
+    t = np.arange(n)
+    x = (0.1 * np.cos(2 * np.pi * 19000 / 240000 * t + 0.9) + 0.02 * rng.standard_normal(n)).astype(np.float32)
+    st0 = np.array([1.5e-4, -0.3, 0.6, 0.8, 1.0, trig0], np.float32)
+    want_x, want_st = orc.pll(x, 19000, 240000, 2.0, 0.0, 0.01, st0)
+    with fmrx.Receiver(0, fmrx.STEREO) as rx:
+        buf = _d(x)
+        st = _d(st0)
+        counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+        rx.debug_pll_stats(counts.data_ptr())
+        torch.cuda.synchronize()
+        rx.pll(buf.data_ptr(), n, 19000, 240000, 2.0, 0.0, 0.01, st.data_ptr())
+        rx.synchronize()
+        rx.debug_pll_stats(None)
+        assert same(buf.cpu().numpy(), want_x)
+        assert same(st.cpu().numpy(), want_st)
+        resumed, checked = counts.cpu().tolist()
+        assert n // 16 - 2 <= checked <= n // 16, checked
+        if hook is not None and hook[0] == "pll_inject":
+            assert resumed > 0, (resumed, checked)
+
+
 @pytest.mark.parametrize("trig0", [131100.0, 300000.0, 700000.0])
 @pytest.mark.parametrize("miss", ["1", "2", "600", "1248", "1249", "5000"])
 def test_pll_index_redo(fmrx, orc, monkeypatch, trig0, miss):

@@ -10,6 +10,10 @@
 #   bench     bench.py without the CPU baseline
 #   pllcnt    the PLL / stereo GPU tests with the count runner on the forms in $CNT (bitmask, default 31)
 #   envab     stage_times per value of $ENVVAR in $VALS ($STARGS: its arguments), alternating, twice
+#   seam      tools/bench_seam.py (per-block fmrx_rf_block + fmrx_audio_block, two contexts, the CLI at --batch 16)
+#   rprof     tools/runner_prof.py per form ($TRIGS) and FMRX_PLL_CNT value ($CNTS), FMRX_AB_PROF build
+#   n2        the N=2 bench line rehearsed with gloo (both ranks on device 0), chunked configs[4] gather
+#   profmono  tools/gpu_bench_prof.sh (bench line, kernel trace, FETCH/WRITE/GRBM passes of the fused kernel)
 #   smoke     __graft_entry__.smoke()
 set -o pipefail
 TAG=${1:-r05}; shift
@@ -45,6 +49,24 @@ for step in "$@"; do
            env $ENVVAR=$v timeout -k 10 300 python tools/stage_times.py $STARGS > $OUT/envab_${r}_$v.json 2>> $OUT/envab.err || { tail $OUT/envab.err; exit 18; }
            echo "$r $ENVVAR=$v $(python tools/stage_summary.py $OUT/envab_${r}_$v.json)"
          done; done ;;
+    seam) timeout -k 10 400 python tools/bench_seam.py > $OUT/bench_seam.json 2> $OUT/bench_seam.err || { tail $OUT/bench_seam.err; exit 19; }
+          cat $OUT/bench_seam.json ;;
+    rprof) # per-form runner timing from the bench stream's real state at each trigOffset in $TRIGS, per
+           # FMRX_PLL_CNT value in $CNTS, with the FMRX_AB_PROF build (chain / evaluator cycles an interval)
+           TR=${TRIGS:-"131072 262144 524288 1048576 2097152"}
+           timeout -k 10 120 python tools/runner_prof.py --save /tmp/rp_states.npz $(for t in $TR; do echo --trig $t; done) \
+               > $OUT/rprof.txt 2>&1 || { tail $OUT/rprof.txt; exit 10; }
+           for c in ${CNTS:-0 31}; do for tr in $TR; do
+             echo "== FMRX_PLL_CNT=$c trig $tr" >> $OUT/rprof.txt
+             FMRX_PLL_CNT=$c FMRX_LIB_PATH=software-defined-radio-course-project_amd/build_ab/libfmrx.so timeout -k 10 120 \
+               python tools/runner_prof.py --load /tmp/rp_states.npz --trig $tr >> $OUT/rprof.txt 2>&1 || { tail $OUT/rprof.txt; exit 10; }
+           done; done
+           grep -v amdgpu.ids $OUT/rprof.txt ;;
+    n2) FMRX_BENCH_BACKEND=gloo timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+          --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 3 --no-cpu-baseline \
+          > $OUT/bench_n2_gloo.json 2> $OUT/bench_n2_gloo.err || { tail $OUT/bench_n2_gloo.err; exit 9; }
+        python -c "import json; j=json.load(open('$OUT/bench_n2_gloo.json')); c=j['baseline_configs']['configs[4]']; print(j['value'], {k: c.get(k) for k in ('seconds', 'seconds_process', 'seconds_gather', 'gather_chunks', 'gather_GBs_after_processing', 'bit_exact_vs_reference')})" ;;
+    profmono) bash tools/gpu_bench_prof.sh $TAG/prof_mono || exit 20 ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail $OUT/smoke.log; exit 5; }
            tail -1 $OUT/smoke.log ;;
   esac
