@@ -316,13 +316,21 @@ def main() -> None:
         dist.destroy_process_group()
 
 
-# Serial-chain floors of the PLL runners (the stereo configs are latency-bound):
-# VALU instructions a step on the runner's critical wave (csrc/pll_pred.hip chain4_3 /
-# chain4_5, pll_idx_kernel, stereo.hip pll_spec_lane_kernel, pll_sat.hip) x ~4.2 cycles a wave64 VALU issue on
-# gfx950 (tools/ubench_dep.hip, profiles/r03/ubench_dep.txt), at the 2.4 GHz peak engine clock
+# Serial-chain floors of the PLL runners (the stereo configs are latency-bound), two
+# per regime: (1) issue: VALU instructions a step on the runner's critical wave (csrc/pll_pred.hip
+# chain4_3 / chain4_5, pll_cnt_kernel, pll_idx_kernel, stereo.hip pll_spec_lane_kernel,
+# pll_sat.hip) x ~4.2 cycles a wave64 VALU issue on gfx950 (tools/ubench_dep.hip); (2) latency:
+# the step's dependent cycles measured with its data in registers (tools/ubench_cnt.hip, one wave,
+# profiles/r05/ubench/ubench_cnt.txt: the index step mode 0, the count step mode 3, the five- and
+# three-candidate asm blocks modes 15 / 16; the lane runner is issue-bound, its latency floor
+# is its issue floor).  Both at the 2.4 GHz peak engine clock.
 CHAIN_VALU_PER_STEP = {"runner_lane": 35.5, "runner_pred": 16.0, "runner_sat": 8.0, "runner_pipe20": 12.0,
                        "runner_pipe21": 12.0, "runner_pipe22": 9.0, "runner_idx17": 11.0, "runner_idx18": 11.0,
-                       "runner_idx19": 11.0}
+                       "runner_idx19": 11.0, "runner_cnt17": 7.0, "runner_cnt18": 7.0, "runner_cnt19": 7.0,
+                       "runner_cnt20": 7.0, "runner_cnt21": 7.0}
+CHAIN_LATENCY_CYCLES = {"runner_pipe20": 57.5, "runner_pipe21": 57.5, "runner_pipe22": 43.0, "runner_idx17": 91.3,
+                        "runner_idx18": 91.3, "runner_idx19": 91.3, "runner_cnt17": 59.8, "runner_cnt18": 59.8,
+                        "runner_cnt19": 59.8, "runner_cnt20": 59.8, "runner_cnt21": 59.8}
 VALU_ISSUE_CYCLES = 4.2
 PEAK_CLOCK_GHZ = 2.4
 
@@ -342,14 +350,18 @@ def stage_latency(rx, run) -> dict:
         if steps > 0 and k in CHAIN_VALU_PER_STEP:
             ns = ms * 1e6 / steps
             floor = CHAIN_VALU_PER_STEP[k] * VALU_ISSUE_CYCLES / PEAK_CLOCK_GHZ
+            lat = max(floor, CHAIN_LATENCY_CYCLES.get(k, 0.0) / PEAK_CLOCK_GHZ)
             regimes[k] = {"steps_per_stream": int(steps), "ns_per_step": round(ns, 2),
-                          "floor_ns_per_step": round(floor, 2), "frac": round(floor / ns, 3)}
+                          "floor_ns_per_step": round(floor, 2), "frac": round(floor / ns, 3),
+                          "latency_floor_ns_per_step": round(lat, 2), "frac_of_latency_floor": round(lat / ns, 3)}
     runner_ms = sum(v[0] for k, v in st.items() if k.startswith("runner_"))
     return {"bound": "serial PLL chain (one recurrence a stream)", "stage_ms": stages,
             "runner_ms": round(runner_ms, 2), "non_runner_ms": round(sum(v[0] for v in st.values()) - runner_ms, 2),
             "regimes": regimes,
-            "floor_note": f"chain VALU a step x {VALU_ISSUE_CYCLES} cycles at {PEAK_CLOCK_GHZ} GHz "
-                          "(bench.CHAIN_VALU_PER_STEP); stage ms from HIP events, overlapping stages add up"}
+            "floor_note": f"floor: chain VALU a step x {VALU_ISSUE_CYCLES} cycles at {PEAK_CLOCK_GHZ} GHz "
+                          "(bench.CHAIN_VALU_PER_STEP); latency_floor: the step's measured dependent cycles with "
+                          "its data in registers (bench.CHAIN_LATENCY_CYCLES, tools/ubench_cnt.hip) at the same "
+                          "clock; stage ms from HIP events, overlapping stages add up"}
 
 
 def cpu_reference_stereo(host_iq, gpu_pcm) -> dict:

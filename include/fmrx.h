@@ -232,7 +232,8 @@ int fmrx_debug_pll_redos(fmrx_ctx* ctx, unsigned* d_counts);
  * n_kinds: 0 RF front end, 1 band-pass pair, 2 PLL pre-pass, 3 lane runner, 4 two-wave          *
  * predicted runner, 5 saturated runner, 6/7/8 three-wave runner forms from trigOffset 2^20 /   *
  * 2^21 / 2^22, 9 check, 10 resume/tail, 11 NCO, 12 audio, 13/14/15 index runner forms from     *
- * trigOffset 2^17 / 2^18 / 2^19.  ms[k] = summed device time,                                   *
+ * trigOffset 2^17 / 2^18 / 2^19, 16-20 count runner forms from 2^17 / 2^18 / 2^19 / 2^20 /      *
+ * 2^21 (FMRX_KNOB_PLL_CNT).  ms[k] = summed device time,                                        *
  * launches[k] = launches, steps[k] = serial PLL steps a runner kind ran as its segment's only  *
  * runner (per stream chain; for ns per step of each regime).  Results are unchanged.           */
 int fmrx_debug_stage_timing(fmrx_ctx* ctx, int op, double* ms, double* steps, long* launches, int n_kinds);

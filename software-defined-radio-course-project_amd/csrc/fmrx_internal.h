@@ -62,7 +62,7 @@ size_t pll_side_doubles(int n, int n_streams);
 // measured, not modelled.
 enum StageKind {
     kStFront, kStBpf, kStPrep, kStLane, kStPred, kStSat, kStPipe20, kStPipe21, kStPipe22, kStCheck, kStTail,
-    kStNco, kStAudio, kStIdx17, kStIdx18, kStIdx19, kStKinds
+    kStNco, kStAudio, kStIdx17, kStIdx18, kStIdx19, kStCnt17, kStCnt18, kStCnt19, kStCnt20, kStCnt21, kStKinds
 };
 struct StageTimer {
     bool on = false;

@@ -60,6 +60,16 @@ __device__ unsigned int g_redo_stream[4][kProfStreams];
 #define PROF_T() 0ull
 #endif
 
+
+// A/B build only (AB=-DFMRX_AB_LDS_PAD=<bytes>): the one-stream-a-workgroup runners reserve that much
+// more LDS, so the dispatcher cannot put two of them on one CU
+#ifdef FMRX_AB_LDS_PAD
+#define FMRX_LDS_PAD()                                             \
+    __shared__ float lds_pad_[FMRX_AB_LDS_PAD / 4];                \
+    asm volatile("" ::"v"((uint32_t)(uintptr_t)&lds_pad_[threadIdx.x & 1]))
+#else
+#define FMRX_LDS_PAD() (void)0
+#endif
 namespace {
 
 // e of a step (input v, 1/v = iv, half turn h = 0.5 [v < 0]) whose previous trigArg is a:
@@ -578,6 +588,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                                                       size_t ostride, int inject, int miss,
                                                       unsigned long long* stats, unsigned* redos) {
     constexpr int NI = NB * BPI;
+    FMRX_LDS_PAD();
     static_assert(NI == 16 || NI == 32 || NI == 64, "the evaluators' lane map: 64 / NI lanes a step");
     static_assert(NC == 3 || NC == 5, "three or five candidates");
     constexpr int LPS = 64 / NI;  // evaluator lanes a step
@@ -1079,6 +1090,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
                float* out_base, size_t ostride, int inject, int miss, float lo, float hi, unsigned long long* stats,
                unsigned* redos) {
     constexpr int NI = 16;          // steps an interval
+    FMRX_LDS_PAD();
     constexpr int SPP = 64 / NC;    // steps a candidate row
     constexpr int NR = NI / SPP;    // candidate rows an interval
     constexpr int HC = NC / 2;      // candidates c0 - HC .. c0 + HC - 1
@@ -1382,6 +1394,7 @@ __global__ void __launch_bounds__(64 * (1 + NW)) __attribute__((amdgpu_waves_per
 pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step, float norm_bw, float* st,
                float* out_base, size_t ostride, int inject, int miss, float lo, float hi, unsigned long long* stats,
                unsigned* redos) {
+    FMRX_LDS_PAD();
     constexpr int NP = NC + 2;  // row slots: T(c_base + l) l <= NC, +inf | NaN, e(c_base + l - 1), NaN
     constexpr int HC = NC / 2;  // candidates c0 - HC .. c0 + HC
     constexpr int RD = 4;       // intervals of step inputs in flight

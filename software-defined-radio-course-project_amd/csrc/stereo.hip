@@ -1057,10 +1057,12 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         const double edge = form == 17 ? 262144.0 : form == 18 ? 524288.0 : form == 19 ? (double)kPllPipeMinLow
                           : form == 20 ? (double)kPllPipeMin5 : form == 21 ? (double)kPllPipeMin : 0.0;
         const size_t e = form == 22 ? (size_t)n : std::min((size_t)(edge - hlo), (size_t)n);
-        const int kind = form == 17 ? kStIdx17 : form == 18 ? kStIdx18 : form == 19 ? kStIdx19
+        const bool cnt = form < 22 && ((kn.cnt >> (form - 17)) & 1) && kPllIdxSimds * n_streams <= n_simd;
+        const int kind = cnt ? kStCnt17 + (form - 17)
+                       : form == 17 ? kStIdx17 : form == 18 ? kStIdx18 : form == 19 ? kStIdx19
                        : form == 20 ? kStPipe20 : form == 21 ? kStPipe21 : kStPipe22;
         timed(kind, (double)(e - j), [&] {
-            if (form < 22 && ((kn.cnt >> (form - 17)) & 1) && kPllIdxSimds * n_streams <= n_simd)
+            if (cnt)
                 idx_rc |= launch_pll_cnt(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j,
                                          (size_t)n, inject, pipe_miss, form, spec_stats, hint.redos);
             else if (form < 20)

@@ -96,7 +96,7 @@ PROTOTYPES = {
 # fmrx_debug_stage_timing's stage kinds (csrc/fmrx_internal.h StageKind)
 STAGES = ["front_end", "bandpass_pair", "pll_prep", "runner_lane", "runner_pred", "runner_sat", "runner_pipe20",
           "runner_pipe21", "runner_pipe22", "pll_check", "pll_tail", "pll_nco", "audio", "runner_idx17", "runner_idx18",
-          "runner_idx19"]
+          "runner_idx19", "runner_cnt17", "runner_cnt18", "runner_cnt19", "runner_cnt20", "runner_cnt21"]
 
 # fmrx_debug_set_knob's knobs (include/fmrx.h FMRX_KNOB_*): none changes the output; the
 # pll_inject / pll_pipe_miss / pll_hint_skew test hooks make the PLL runners redo work

@@ -14,6 +14,7 @@
 #   rprof     tools/runner_prof.py per form ($TRIGS) and FMRX_PLL_CNT value ($CNTS), FMRX_AB_PROF build
 #   n2        the N=2 bench line rehearsed with gloo (both ranks on device 0), chunked configs[4] gather
 #   profmono  tools/gpu_bench_prof.sh (bench line, kernel trace, FETCH/WRITE/GRBM passes of the fused kernel)
+#   libab     stage_times per library in $LIBS (A/B builds), alternating, twice
 #   smoke     __graft_entry__.smoke()
 set -o pipefail
 TAG=${1:-r05}; shift
@@ -67,6 +68,13 @@ for step in "$@"; do
           > $OUT/bench_n2_gloo.json 2> $OUT/bench_n2_gloo.err || { tail $OUT/bench_n2_gloo.err; exit 9; }
         python -c "import json; j=json.load(open('$OUT/bench_n2_gloo.json')); c=j['baseline_configs']['configs[4]']; print(j['value'], {k: c.get(k) for k in ('seconds', 'seconds_process', 'seconds_gather', 'gather_chunks', 'gather_GBs_after_processing', 'bit_exact_vs_reference')})" ;;
     profmono) bash tools/gpu_bench_prof.sh $TAG/prof_mono || exit 20 ;;
+    libab) # stage_times with each library in $LIBS (package-relative .so paths), alternating, twice
+         for r in 1 2; do for lib in ${LIBS:-libfmrx.so}; do
+           tagl=$(echo $lib | tr / _)
+           FMRX_LIB_PATH=software-defined-radio-course-project_amd/$lib timeout -k 10 300 python tools/stage_times.py $STARGS \
+             > $OUT/libab_${r}_$tagl.json 2>> $OUT/libab.err || { tail $OUT/libab.err; exit 16; }
+           echo "$r $lib $(python tools/stage_summary.py $OUT/libab_${r}_$tagl.json)"
+         done; done ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail $OUT/smoke.log; exit 5; }
            tail -1 $OUT/smoke.log ;;
   esac

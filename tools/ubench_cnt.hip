@@ -25,7 +25,11 @@
 //            suffix), e = v_readfirstlane(E) (the lowest active lane holds the chosen e),
 //            EXEC restored, (Ki e, Kp e) with e an SGPR, three updates; s_nop 4 after the cmpx;
 //   mode 13: mode 12 with s_nop 0 after the cmpx (timing only if the hazard needs more);
-//   mode 14: mode 12 with (Ki e, Kp e) precomputed (two v_readfirstlane, no multiply).
+//   mode 14: mode 12 with (Ki e, Kp e) precomputed (two v_readfirstlane, no multiply);
+//   mode 15: pll_pipe_kernel's five-candidate step as its four-step asm block (chain4_5: four
+//            compares into SGPR masks, four v_cndmask, v_pk_mul_f32 with (Ki, Kp) in SGPRs, three
+//            updates);
+//   mode 16: the three-candidate step as its four-step asm block (chain4_3).
 // Prints shader cycles (s_memtime) per step.
 //
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o tools/ubench_cnt tools/ubench_cnt.hip
@@ -114,6 +118,28 @@ constexpr int NB = 16;
                    [f3] "v"(F[q + 3])                                                                     \
                  : "s40", "s41", "s42", "s44", "s45", "v254", "v255", "exec")
 
+// pll_pred.hip's chain blocks (FMRX_CHAIN_STEP3 / STEP5), verbatim
+#define PT_TAIL(P, Q)                                            \
+    "v_pk_mul_f32 v[254:255], v[252:253], %[kk] op_sel_hi:[0,1]\n" \
+    "v_add_f32 %[ig], %[ig], v254\n"                             \
+    "v_add_f32 v255, v255, %[ig]\n"                              \
+    "v_add_f32 " Q ", " P ", v255\n"
+#define PT_STEP3(P, Q, K)                                  \
+    "v_cmp_ge_f32_e64 %[m0], " P ", %[ta" #K "]\n"           \
+    "v_cmp_ge_f32_e64 %[m1], " P ", %[tb" #K "]\n"           \
+    "s_nop 0\n"                                            \
+    "v_cndmask_b32_e64 v252, %[ea" #K "], %[eb" #K "], %[m0]\n" \
+    "v_cndmask_b32_e64 v252, v252, %[ec" #K "], %[m1]\n" PT_TAIL(P, Q)
+#define PT_STEP5(P, Q, K)                                  \
+    "v_cmp_ge_f32_e64 %[m0], " P ", %[ta" #K "]\n"           \
+    "v_cmp_ge_f32_e64 %[m1], " P ", %[tb" #K "]\n"           \
+    "v_cmp_ge_f32_e64 %[m2], " P ", %[tc" #K "]\n"           \
+    "v_cmp_ge_f32_e64 %[m3], " P ", %[td" #K "]\n"           \
+    "v_cndmask_b32_e64 v252, %[ea" #K "], %[eb" #K "], %[m0]\n" \
+    "v_cndmask_b32_e64 v252, v252, %[ec" #K "], %[m1]\n"     \
+    "v_cndmask_b32_e64 v252, v252, %[ed" #K "], %[m2]\n"     \
+    "v_cndmask_b32_e64 v252, v252, %[ee" #K "], %[m3]\n" PT_TAIL(P, Q)
+
 template <int MODE>
 __global__ void __launch_bounds__(256) chain(float* out, long long* cyc, int nb, int busy) {
     const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
@@ -164,7 +190,51 @@ __global__ void __launch_bounds__(256) chain(float* out, long long* cyc, int nb,
                 else
                     ASM4(EXEC_STEP_PRE);
                 phase = p4;
-                acc += p1 * 0.0f + p2 * 0.0f + p3 * 0.0f;
+                (void)p1;
+                (void)p2;
+                (void)p3;
+            }
+        } else if constexpr (MODE == 15 || MODE == 16) {
+            const uint64_t skk = (uint64_t)__builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, Ki)) |
+                                 ((uint64_t)__builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, Kp)) << 32);
+#pragma unroll
+            for (int q = 0; q < NB; q += 4) {
+                float p1, p2, p3, p4;
+                uint64_t m0, m1, m2, m3;
+                auto Tq = [&](int u, int d) { return T[(q + u + d) % NB]; };
+                auto Eq = [&](int u, int d) { return E[(q + u + d) % NB]; };
+                if constexpr (MODE == 15)
+                    asm volatile(PT_STEP5("%[p]", "%[q1]", 0) PT_STEP5("%[q1]", "%[q2]", 1) PT_STEP5("%[q2]", "%[q3]", 2)
+                                     PT_STEP5("%[q3]", "%[q4]", 3)
+                                 : [q1] "=&v"(p1), [q2] "=&v"(p2), [q3] "=&v"(p3), [q4] "=&v"(p4), [ig] "+v"(integ),
+                                   [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3)
+                                 : [p] "v"(phase), [kk] "s"(skk),
+                                   [ta0] "v"(Tq(0, 0)), [tb0] "v"(Tq(0, 1)), [tc0] "v"(Tq(0, 2)), [td0] "v"(Tq(0, 3)),
+                                   [ea0] "v"(Eq(0, 0)), [eb0] "v"(Eq(0, 1)), [ec0] "v"(Eq(0, 2)), [ed0] "v"(Eq(0, 3)), [ee0] "v"(Eq(0, 4)),
+                                   [ta1] "v"(Tq(1, 0)), [tb1] "v"(Tq(1, 1)), [tc1] "v"(Tq(1, 2)), [td1] "v"(Tq(1, 3)),
+                                   [ea1] "v"(Eq(1, 0)), [eb1] "v"(Eq(1, 1)), [ec1] "v"(Eq(1, 2)), [ed1] "v"(Eq(1, 3)), [ee1] "v"(Eq(1, 4)),
+                                   [ta2] "v"(Tq(2, 0)), [tb2] "v"(Tq(2, 1)), [tc2] "v"(Tq(2, 2)), [td2] "v"(Tq(2, 3)),
+                                   [ea2] "v"(Eq(2, 0)), [eb2] "v"(Eq(2, 1)), [ec2] "v"(Eq(2, 2)), [ed2] "v"(Eq(2, 3)), [ee2] "v"(Eq(2, 4)),
+                                   [ta3] "v"(Tq(3, 0)), [tb3] "v"(Tq(3, 1)), [tc3] "v"(Tq(3, 2)), [td3] "v"(Tq(3, 3)),
+                                   [ea3] "v"(Eq(3, 0)), [eb3] "v"(Eq(3, 1)), [ec3] "v"(Eq(3, 2)), [ed3] "v"(Eq(3, 3)), [ee3] "v"(Eq(3, 4))
+                                 : "v252", "v253", "v254", "v255");
+                else
+                    asm volatile(PT_STEP3("%[p]", "%[q1]", 0) PT_STEP3("%[q1]", "%[q2]", 1) PT_STEP3("%[q2]", "%[q3]", 2)
+                                     PT_STEP3("%[q3]", "%[q4]", 3)
+                                 : [q1] "=&v"(p1), [q2] "=&v"(p2), [q3] "=&v"(p3), [q4] "=&v"(p4), [ig] "+v"(integ),
+                                   [m0] "=&s"(m0), [m1] "=&s"(m1)
+                                 : [p] "v"(phase), [kk] "s"(skk),
+                                   [ta0] "v"(Tq(0, 0)), [tb0] "v"(Tq(0, 1)), [ea0] "v"(Eq(0, 0)), [eb0] "v"(Eq(0, 1)), [ec0] "v"(Eq(0, 2)),
+                                   [ta1] "v"(Tq(1, 0)), [tb1] "v"(Tq(1, 1)), [ea1] "v"(Eq(1, 0)), [eb1] "v"(Eq(1, 1)), [ec1] "v"(Eq(1, 2)),
+                                   [ta2] "v"(Tq(2, 0)), [tb2] "v"(Tq(2, 1)), [ea2] "v"(Eq(2, 0)), [eb2] "v"(Eq(2, 1)), [ec2] "v"(Eq(2, 2)),
+                                   [ta3] "v"(Tq(3, 0)), [tb3] "v"(Tq(3, 1)), [ea3] "v"(Eq(3, 0)), [eb3] "v"(Eq(3, 1)), [ec3] "v"(Eq(3, 2))
+                                 : "v252", "v253", "v254", "v255");
+                phase = p4;
+                (void)m2;
+                (void)m3;
+                (void)p1;
+                (void)p2;
+                (void)p3;
             }
         } else if constexpr (MODE == 11) {
 #pragma unroll
@@ -214,7 +284,9 @@ __global__ void __launch_bounds__(256) chain(float* out, long long* cyc, int nb,
                                    [e2] "v"(E[q + 2]), [e3] "v"(E[q + 3])
                                  : "s40", "s41", "s42", "s44", "s45", "v254", "v255");
                 phase = p4;
-                acc += p1 * 0.0f + p2 * 0.0f + p3 * 0.0f;
+                (void)p1;
+                (void)p2;
+                (void)p3;
             }
         } else if constexpr (MODE == 7) {
 #pragma unroll
@@ -300,9 +372,9 @@ int main() {
     long long* d_cyc;
     (void)hipMalloc(&d_out, 1024 * 4);
     (void)hipMalloc(&d_cyc, 8);
-    run_all(1, 0, d_out, d_cyc, std::make_integer_sequence<int, 15>{});
-    run_all(4, 0, d_out, d_cyc, std::make_integer_sequence<int, 15>{});
-    run_all(4, 1, d_out, d_cyc, std::make_integer_sequence<int, 15>{});
+    run_all(1, 0, d_out, d_cyc, std::make_integer_sequence<int, 17>{});
+    run_all(4, 0, d_out, d_cyc, std::make_integer_sequence<int, 17>{});
+    run_all(4, 1, d_out, d_cyc, std::make_integer_sequence<int, 17>{});
     (void)hipFree(d_out);
     (void)hipFree(d_cyc);
     return 0;
