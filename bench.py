@@ -327,10 +327,10 @@ def main() -> None:
 CHAIN_VALU_PER_STEP = {"runner_lane": 35.5, "runner_pred": 16.0, "runner_sat": 8.0, "runner_pipe20": 12.0,
                        "runner_pipe21": 12.0, "runner_pipe22": 9.0, "runner_idx17": 11.0, "runner_idx18": 11.0,
                        "runner_idx19": 11.0, "runner_cnt17": 7.0, "runner_cnt18": 7.0, "runner_cnt19": 7.0,
-                       "runner_cnt20": 7.0, "runner_cnt21": 7.0}
+                       "runner_cnt20": 7.0, "runner_cnt21": 7.0, "runner_stick": 9.0}
 CHAIN_LATENCY_CYCLES = {"runner_pipe20": 57.5, "runner_pipe21": 57.5, "runner_pipe22": 43.0, "runner_idx17": 91.3,
                         "runner_idx18": 91.3, "runner_idx19": 91.3, "runner_cnt17": 59.8, "runner_cnt18": 59.8,
-                        "runner_cnt19": 59.8, "runner_cnt20": 59.8, "runner_cnt21": 59.8}
+                        "runner_cnt19": 59.8, "runner_cnt20": 59.8, "runner_cnt21": 59.8, "runner_stick": 43.0}
 VALU_ISSUE_CYCLES = 4.2
 PEAK_CLOCK_GHZ = 2.4
 

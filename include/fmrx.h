@@ -233,7 +233,8 @@ int fmrx_debug_pll_redos(fmrx_ctx* ctx, unsigned* d_counts);
  * predicted runner, 5 saturated runner, 6/7/8 three-wave runner forms from trigOffset 2^20 /   *
  * 2^21 / 2^22, 9 check, 10 resume/tail, 11 NCO, 12 audio, 13/14/15 index runner forms from     *
  * trigOffset 2^17 / 2^18 / 2^19, 16-20 count runner forms from 2^17 / 2^18 / 2^19 / 2^20 /      *
- * 2^21 (FMRX_KNOB_PLL_CNT).  ms[k] = summed device time,                                        *
+ * 2^21 (FMRX_KNOB_PLL_CNT), 21 the three-candidate stick form (trigOffset stuck at 2^24).      *
+ * ms[k] = summed device time,                                                                    *
  * launches[k] = launches, steps[k] = serial PLL steps a runner kind ran as its segment's only  *
  * runner (per stream chain; for ns per step of each regime).  Results are unchanged.           */
 int fmrx_debug_stage_timing(fmrx_ctx* ctx, int op, double* ms, double* steps, long* launches, int n_kinds);
@@ -257,6 +258,8 @@ int fmrx_debug_stage_timing(fmrx_ctx* ctx, int op, double* ms, double* steps, lo
 #define FMRX_KNOB_PLL_PIPE_MISS 10    /* test hook: self-certifying runners miss interval k            */
 #define FMRX_KNOB_PLL_HINT_SKEW 11    /* test hook: host trigOffset bounds shifted by value samples    */
 #define FMRX_KNOB_PLL_CNT 12          /* bit f-17: count runner for form f's range (12)   FMRX_PLL_CNT  */
+#define FMRX_KNOB_PLL_STICK 13        /* 1: the stick form past trigOffset 2^24         FMRX_PLL_STICK */
+#define FMRX_KNOB_STEREO_HEAD 14      /* first chunk in 16ths of a chunk (8)          FMRX_STEREO_HEAD */
 int fmrx_debug_set_knob(fmrx_ctx* ctx, int knob, double value);
 
 #ifdef __cplusplus

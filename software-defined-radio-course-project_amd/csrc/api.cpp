@@ -134,6 +134,7 @@ struct fmrx_ctx {
     struct Knobs {
         PllKnobs pll;
         int stereo_chunks = 0;  // 0: by stream count and call length; k: k chunks (1: serial engine)
+        int stereo_head = 8;    // the first chunk's blocks in 16ths of a middle chunk's
         int mono_split = -1;    // -1: kOlderShare; 0: equal spans; n: the older wave's n / 1024
         int bpf_tile = 1;       // 0: the per-output band-pass kernel
         int halo_kernel = 0;    // 1: the separate halo_kernel after the fused one
@@ -476,6 +477,17 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
     return 0;
 }
 
+// First block of chunk k of K (k = K: n_blocks).  The last chunk is half the others and the first
+// head / 16 of one (knob stereo_head, default 8: half): the first chunk's front end and the last
+// chunk's NCO and audio stage have no PLL beside them.
+size_t chunk_begin(size_t n_blocks, int k, int K, int head = 8) {
+    if (K <= 1 || k <= 0) return k <= 0 ? 0 : n_blocks;
+    if (k >= K) return n_blocks;
+    const unsigned long long h = (unsigned long long)std::max(1, std::min(head, 64));
+    return (size_t)(((unsigned long long)n_blocks * (h + 16ULL * (unsigned long long)(k - 1))) /
+                    (h + 16ULL * (unsigned long long)(K - 2) + 8ULL));
+}
+
 // Chunks of the stereo pipeline for a call of n_blocks blocks a stream: the stage work beside
 // the serial PLL (front end, band-pass pair, NCO, audio) grows with the streams, the PLL's with
 // the samples a stream, so a call pipelines from 16 streams on when a chunk holds enough blocks.
@@ -488,18 +500,16 @@ int stereo_chunks(const fmrx_ctx* c, size_t n_blocks) {
     // a chunk past the first reads its RF halo from the call's own bytes in front of it: every
     // chunk holds at least the halo's blocks
     const size_t hb = (c->halo_bytes + c->geo.block_bytes - 1) / c->geo.block_bytes;
-    while (k > 1 && n_blocks / (2 * (size_t)(k - 1)) < hb) k--;  // the half-size end chunks too
+    auto short_chunk = [&](int kk) {  // a chunk of the partition shorter than the halo
+        for (int j = 0; j < kk; j++)
+            if (chunk_begin(n_blocks, j + 1, kk, c->knobs.stereo_head) - chunk_begin(n_blocks, j, kk, c->knobs.stereo_head) < hb)
+                return true;
+        return false;
+    };
+    while (k > 1 && short_chunk(k)) k--;  // the short first and last chunks too
     return k;
 }
 
-// First block of chunk k of K (k = K: n_blocks).  The first and the last chunk are half the
-// others: the first chunk's front end and the last chunk's NCO and audio stage have no PLL
-// beside them.
-size_t chunk_begin(size_t n_blocks, int k, int K) {
-    if (K <= 1 || k <= 0) return k <= 0 ? 0 : n_blocks;
-    if (k >= K) return n_blocks;
-    return (size_t)(((unsigned long long)n_blocks * (unsigned long long)(2 * k - 1)) / (2ULL * (K - 1)));
-}
 
 // The stereo engine over the call's blocks in K chunks, pipelined like project.cpp's two threads
 // and their queue (rf_thread / audio_thread, project.cpp:17,71-80,133-141): the context stream
@@ -537,7 +547,7 @@ int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks,
     const int ns = c->cfg.n_streams;
     const size_t ipb = c->geo.if_samples, n_if = n_blocks * ipb;
     for (int k = 0; k < K; k++)
-        if ((chunk_begin(n_blocks, k + 1, K) - chunk_begin(n_blocks, k, K)) * c->geo.block_bytes < c->halo_bytes)
+        if ((chunk_begin(n_blocks, k + 1, K, c->knobs.stereo_head) - chunk_begin(n_blocks, k, K, c->knobs.stereo_head)) * c->geo.block_bytes < c->halo_bytes)
             return fail(FMRX_EINVAL, "chunks shorter than the halo");
     int rc = c->d_channel.ensure(n_if * ns);
     if (!rc) rc = c->d_carrier.ensure(n_if * ns);
@@ -564,7 +574,7 @@ int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks,
     HIPCHK(hipStreamWaitEvent(c->s_audio, ev_start, 0));
     size_t max_m = 0;
     for (int k = 0; k < K; k++)
-        max_m = std::max(max_m, (chunk_begin(n_blocks, k + 1, K) - chunk_begin(n_blocks, k, K)) * ipb);
+        max_m = std::max(max_m, (chunk_begin(n_blocks, k + 1, K, c->knobs.stereo_head) - chunk_begin(n_blocks, k, K, c->knobs.stereo_head)) * ipb);
     if ((rc = c->d_pll_side.ensure(pll_side_doubles((int)max_m, ns)))) return rc;
     if ((rc = c->d_pll_side2.ensure(pll_side_doubles((int)max_m, ns)))) return rc;
     AudioLaunch A{};
@@ -606,7 +616,7 @@ int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks,
         return 0;
     };
     for (int k = 0; k < K; k++) {
-        const size_t b0 = chunk_begin(n_blocks, k, K), b1 = chunk_begin(n_blocks, k + 1, K);
+        const size_t b0 = chunk_begin(n_blocks, k, K, c->knobs.stereo_head), b1 = chunk_begin(n_blocks, k + 1, K, c->knobs.stereo_head);
         const size_t nb = b1 - b0, m = nb * ipb, off = b0 * ipb;
         const bool last = k == K - 1;
         if (k == 1 && lane_m > 0) HIPCHK(hipStreamWaitEvent(c->s_front, ev_lane, 0));
@@ -751,7 +761,9 @@ static fmrx_ctx::Knobs knobs_from_env() {
     k.pll.pipe = get("FMRX_PLL_PIPE", 1);
     k.pll.idx = get("FMRX_PLL_IDX", 2);
     k.pll.cnt = get("FMRX_PLL_CNT", kPllCntDefault);
+    k.pll.stick = get("FMRX_PLL_STICK", 1);
     k.stereo_chunks = std::max(0, get("FMRX_STEREO_CHUNKS", 0));
+    k.stereo_head = std::max(1, get("FMRX_STEREO_HEAD", 8));
     k.mono_split = get("FMRX_MONO_SPLIT", -1);
     k.bpf_tile = get("FMRX_BPF_TILE", 1);
     k.halo_kernel = get("FMRX_HALO_KERNEL", 0);
@@ -1456,6 +1468,7 @@ int fmrx_debug_set_knob(fmrx_ctx* c, int knob, double value) {
         case FMRX_KNOB_PLL_PIPE: k.pll.pipe = v; break;
         case FMRX_KNOB_PLL_IDX: k.pll.idx = v; break;
         case FMRX_KNOB_STEREO_CHUNKS: k.stereo_chunks = std::max(0, v); break;
+        case FMRX_KNOB_STEREO_HEAD: k.stereo_head = std::max(1, v); break;
         case FMRX_KNOB_MONO_SPLIT: k.mono_split = v; break;
         case FMRX_KNOB_BPF_TILE: k.bpf_tile = v; break;
         case FMRX_KNOB_HALO_KERNEL: k.halo_kernel = v; break;
@@ -1463,6 +1476,7 @@ int fmrx_debug_set_knob(fmrx_ctx* c, int knob, double value) {
         case FMRX_KNOB_PLL_PIPE_MISS: k.pll.pipe_miss = v; break;
         case FMRX_KNOB_PLL_HINT_SKEW: k.pll.skew = value; break;
         case FMRX_KNOB_PLL_CNT: k.pll.cnt = v; break;
+        case FMRX_KNOB_PLL_STICK: k.pll.stick = v; break;
         default: return fail(FMRX_EINVAL, "unknown knob %d", knob);
     }
     return FMRX_OK;

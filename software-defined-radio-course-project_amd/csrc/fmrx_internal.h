@@ -62,7 +62,7 @@ size_t pll_side_doubles(int n, int n_streams);
 // measured, not modelled.
 enum StageKind {
     kStFront, kStBpf, kStPrep, kStLane, kStPred, kStSat, kStPipe20, kStPipe21, kStPipe22, kStCheck, kStTail,
-    kStNco, kStAudio, kStIdx17, kStIdx18, kStIdx19, kStCnt17, kStCnt18, kStCnt19, kStCnt20, kStCnt21, kStKinds
+    kStNco, kStAudio, kStIdx17, kStIdx18, kStIdx19, kStCnt17, kStCnt18, kStCnt19, kStCnt20, kStCnt21, kStStick, kStKinds
 };
 struct StageTimer {
     bool on = false;
@@ -110,6 +110,7 @@ struct PllKnobs {
     int pipe = 1;        // 0: no three-wave runner (FMRX_PLL_PIPE)
     int idx = 2;         // index runner from 2^17 (2), from 2^18 (1), off (0) (FMRX_PLL_IDX)
     int cnt = 12;        // bit f - 17: the count runner takes form f's range (FMRX_PLL_CNT; kPllCntDefault)
+    int stick = 1;       // the three-candidate runner's stick form past trigOffset 2^24 (FMRX_PLL_STICK)
     int inject = -1;     // test hook: the runners corrupt batch 1 + (k + s) % (nb - 1) of stream s
     int pipe_miss = -1;  // test hook: the self-certifying runners report interval k as missed
     double skew = 0.0;   // test hook: the host's trigOffset bounds shifted by this many samples

@@ -61,14 +61,13 @@ __device__ unsigned int g_redo_stream[4][kProfStreams];
 #endif
 
 
-// A/B build only (AB=-DFMRX_AB_LDS_PAD=<bytes>): the one-stream-a-workgroup runners reserve that much
-// more LDS, so the dispatcher cannot put two of them on one CU
-#ifdef FMRX_AB_LDS_PAD
-#define FMRX_LDS_PAD()                                             \
-    __shared__ float lds_pad_[FMRX_AB_LDS_PAD / 4];                \
-    asm volatile("" ::"v"((uint32_t)(uintptr_t)&lds_pad_[threadIdx.x & 1]))
+// A/B build only (AB=-DFMRX_AB_V256): the CU-a-stream runners (index, count) take 256 VGPRs a wave,
+// so a SIMD holds two of their waves and a CU one five-wave workgroup: two streams' chains can
+// then not be placed on one CU
+#ifdef FMRX_AB_V256
+#define FMRX_ONE_WG_A_CU() asm volatile("" ::: "v255")
 #else
-#define FMRX_LDS_PAD() (void)0
+#define FMRX_ONE_WG_A_CU() (void)0
 #endif
 namespace {
 
@@ -582,15 +581,19 @@ __device__ __noinline__ float exact_e(float a, float v) {
 // keeps each burst of reads whole instead of threading it through the steps for occupancy.
 // io / out: the stream's input and trigArg rows from the range's first sample (stride / ostride
 // floats a stream), n samples; st: the state (read at the start, the exact end state written).
-template <int NB, int BPI, int RD, int NC>
+template <int NB, int BPI, int RD, int NC, bool STK = false>
 __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))) pll_pipe_kernel(const float* io, int n, int n_streams, size_t stride,
                                                       double step, float norm_bw, float* st, float* out_base,
                                                       size_t ostride, int inject, int miss,
                                                       unsigned long long* stats, unsigned* redos) {
     constexpr int NI = NB * BPI;
-    FMRX_LDS_PAD();
     static_assert(NI == 16 || NI == 32 || NI == 64, "the evaluators' lane map: 64 / NI lanes a step");
     static_assert(NC == 3 || NC == 5, "three or five candidates");
+    // STK: the stuck trigOffset (2^24, filter.cpp:165-166: 69.9 s into a stream).  Every step's
+    // P is then the same, so c0 = float(P + phase_ref) and the two thresholds are the interval's
+    // constants: wave 2 forms them once (sthr) and the e of the three candidates sit three floats a
+    // step (sek) -- 0.75 16-byte reads a step for the chain instead of 1.25
+    static_assert(!STK || (NC == 3 && BPI > 1), "the stick form is the three-candidate replay form");
     constexpr int LPS = 64 / NI;  // evaluator lanes a step
     constexpr int HC = NC / 2;    // candidates c0 - HC .. c0 + HC
     // the chain's steps a burst of reads (its registers hold a burst's data)
@@ -617,6 +620,22 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     constexpr bool REPLAY = BPI > 1;
     __shared__ float sph[REPLAY ? 1 : 4][REPLAY ? 1 : NI];
     __shared__ int smiss[4], sexact[4];
+    __shared__ float sek[STK ? 4 : 1][STK ? 3 * NI : 4];
+    __shared__ float2 sthr[4];
+    // the candidate data the chain and the replay select from at step J of ring slot sl: (T0, T1,
+    // e(c0 - 1), e(c0)) and e(c0 + 1)
+    auto cand = [&](int sl, int J) {
+        if constexpr (STK) {
+            const float2 T = sthr[sl];
+            return make_float4(T.x, T.y, sek[STK ? sl : 0][STK ? 3 * J : 0], sek[STK ? sl : 0][STK ? 3 * J + 1 : 0]);
+        } else {
+            return sel[sl][J];
+        }
+    };
+    auto cand_ep = [&](int sl, int J) {
+        if constexpr (STK) return sek[STK ? sl : 0][STK ? 3 * J + 2 : 0];
+        else return sep[sl][J];
+    };
     // the wave (readfirstlane: uniform, so the waves' branches and loops are scalar)
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63, l = t & (NI - 1), h = t / NI;
     const int s = blockIdx.x;  // grid = n_streams
@@ -631,7 +650,8 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     PllState p{uni(S[0]), uni(S[1]), uni(S[2]), uni(S[3]), uni(S[5])};
     // the variant's domain (uniform over the group): NC = 3 from 2^22; NC = 5 with 64-step
     // intervals in [2^21, 2^22), with 16-step ones in [2^20, 2^21)
-    const bool in_domain = NC == 3 ? pll_pipe_stream(p.trig, step, kPllPipeMin)
+    const bool in_domain = STK ? pll_pipe_stream(p.trig, step, kPllTrigStick)
+                         : NC == 3 ? pll_pipe_stream(p.trig, step, kPllPipeMin)
                                    : NI == 64 ? pll_pipe_stream(p.trig, step, kPllPipeMin5, kPllPipeMin - 1.0f)
                                               : pll_pipe_stream(p.trig, step, kPllPipeMinLow, kPllPipeMin5 - 1.0f);
     const float trig0 = p.trig;
@@ -697,13 +717,19 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                     bool ok;
                     const float e = pred_e_cert(__builtin_bit_cast(float, cb + (uint32_t)(r - HC)), v, iv, ok);
                     scert[sl][l][r] = ok ? 1 : 0;
-                    if (r == NC - 1) sep[sl][l] = e;
+                    if (STK) sek[STK ? sl : 0][STK ? 3 * l + r : 0] = e;
+                    else if (r == NC - 1) sep[sl][l] = e;
                     else if (NC == 3) reinterpret_cast<float*>(&sel[sl][l])[2 + r] = e;
                     else reinterpret_cast<float*>(&sel2[NC == 5 ? sl : 0][NC == 5 ? l : 0])[r] = e;
                 }
             } else {
-                for (int r = h; r < NC - 1; r += LPS)
-                    reinterpret_cast<float*>(&sel[sl][l])[r] = phase_thr(pr, cb + (uint32_t)(r + 1 - HC));
+                if (STK) {  // the interval's two thresholds (every step's P and c0 are the same)
+                    if (h == 0 && l == 0)
+                        sthr[sl] = make_float2(phase_thr(pr, cb + (uint32_t)(1 - HC)), phase_thr(pr, cb + (uint32_t)(2 - HC)));
+                } else {
+                    for (int r = h; r < NC - 1; r += LPS)
+                        reinterpret_cast<float*>(&sel[sl][l])[r] = phase_thr(pr, cb + (uint32_t)(r + 1 - HC));
+                }
                 if (h == 0) {
                     scb[sl][l] = cb - (uint32_t)HC;
                     spr[sl][l] = pr;
@@ -720,7 +746,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         // an LDS store of four phases cost it ~20 cycles.)
         auto verdict = [&](int sl, int J, float a) {
             const uint32_t cm = scb[sl][J];
-            const float4 tt = sel[sl][J];
+            const float4 tt = cand(sl, J);
             const float c0 = __builtin_bit_cast(float, cm + (uint32_t)HC);
             const bool thr_ok = tt.x > -__builtin_inff() && tt.y > -__builtin_inff() &&
                                 (NC == 3 || (tt.z > -__builtin_inff() && tt.w > -__builtin_inff()));
@@ -764,8 +790,8 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             float4 ca, ca2;
             float cep;
             if (gb > 0) {
-                ca = sel[sl][NB * gb - 1];
-                cep = sep[sl][NB * gb - 1];
+                ca = cand(sl, NB * gb - 1);
+                cep = cand_ep(sl, NB * gb - 1);
                 ca2 = sel2[NC == 5 ? sl : 0][NC == 5 ? NB * gb - 1 : 0];
             } else if (sexact[(k - 1) & 3]) {
                 const int j = j0(k);
@@ -774,8 +800,8 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 ca2 = make_float4(e, e, e, e);
                 cep = e;
             } else {
-                ca = sel[(k - 1) & 3][NI - 1];
-                cep = sep[(k - 1) & 3][NI - 1];
+                ca = cand((k - 1) & 3, NI - 1);
+                cep = cand_ep((k - 1) & 3, NI - 1);
                 ca2 = sel2[NC == 5 ? (k - 1) & 3 : 0][NC == 5 ? NI - 1 : 0];
             }
             // the batch's candidate data, read before the steps (the step loop then never waits on
@@ -784,8 +810,8 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             float dep[NB];
 #pragma unroll
             for (int j = 0; j < NB - 1; j++) {
-                da[j] = sel[sl][NB * gb + j];
-                dep[j] = sep[sl][NB * gb + j];
+                da[j] = cand(sl, NB * gb + j);
+                dep[j] = cand_ep(sl, NB * gb + j);
                 if constexpr (NC == 5) da2[j] = sel2[NC == 5 ? sl : 0][NC == 5 ? NB * gb + j : 0];
             }
             // pll_batch_fast's range test, on the state at the batch's start
@@ -916,13 +942,30 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         unroll_ic(
             [&](auto hc) {
                 constexpr int H = decltype(hc)::value;
+                if constexpr (STK) {  // three 16-byte reads a group of four steps, the thresholds once
+                    const float2 T = sthr[is];
 #pragma unroll
-                for (int q = 0; q < CH / 4; q++) {
-                    *reinterpret_cast<float4*>(&EP[4 * q]) = reinterpret_cast<const float4*>(&sep[is][H * CH])[q];
+                    for (int q = 0; q < CH / 4; q++) {
+                        float ek[12];
 #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        A[4 * q + u] = sel[is][H * CH + 4 * q + u];
-                        if constexpr (NC == 5) A2[4 * q + u] = sel2[NC == 5 ? is : 0][NC == 5 ? H * CH + 4 * q + u : 0];
+                        for (int u = 0; u < 3; u++)
+                            *reinterpret_cast<float4*>(&ek[4 * u]) =
+                                reinterpret_cast<const float4*>(&sek[STK ? is : 0][STK ? 3 * H * CH : 0])[3 * q + u];
+#pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            A[4 * q + u] = make_float4(T.x, T.y, ek[3 * u], ek[3 * u + 1]);
+                            EP[4 * q + u] = ek[3 * u + 2];
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < CH / 4; q++) {
+                        *reinterpret_cast<float4*>(&EP[4 * q]) = reinterpret_cast<const float4*>(&sep[is][H * CH])[q];
+#pragma unroll
+                        for (int u = 0; u < 4; u++) {
+                            A[4 * q + u] = sel[is][H * CH + 4 * q + u];
+                            if constexpr (NC == 5) A2[4 * q + u] = sel2[NC == 5 ? is : 0][NC == 5 ? H * CH + 4 * q + u : 0];
+                        }
                     }
                 }
                 float2 brec[CH / NB];  // (integ, phase) at the end of each batch of the burst
@@ -1090,7 +1133,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
                float* out_base, size_t ostride, int inject, int miss, float lo, float hi, unsigned long long* stats,
                unsigned* redos) {
     constexpr int NI = 16;          // steps an interval
-    FMRX_LDS_PAD();
+    FMRX_ONE_WG_A_CU();
     constexpr int SPP = 64 / NC;    // steps a candidate row
     constexpr int NR = NI / SPP;    // candidate rows an interval
     constexpr int HC = NC / 2;      // candidates c0 - HC .. c0 + HC - 1
@@ -1394,7 +1437,7 @@ __global__ void __launch_bounds__(64 * (1 + NW)) __attribute__((amdgpu_waves_per
 pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step, float norm_bw, float* st,
                float* out_base, size_t ostride, int inject, int miss, float lo, float hi, unsigned long long* stats,
                unsigned* redos) {
-    FMRX_LDS_PAD();
+    FMRX_ONE_WG_A_CU();
     constexpr int NP = NC + 2;  // row slots: T(c_base + l) l <= NC, +inf | NaN, e(c_base + l - 1), NaN
     constexpr int HC = NC / 2;  // candidates c0 - HC .. c0 + HC
     constexpr int RD = 4;       // intervals of step inputs in flight
@@ -1736,7 +1779,10 @@ void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_
     reg_pred_prof();
 #endif
     if (n <= 0) return;
-    if (form == 22)
+    if (form == 23)
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8, 3, true>), dim3(n_streams), dim3(192), 0, s, io, n,
+                           n_streams, stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
+    else if (form == 22)
         hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8, 3>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
                            stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
     else if (form == 21)

@@ -1052,15 +1052,19 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     int idx_rc = 0;
     for (size_t j = n_seg; pipe && j < (size_t)n;) {
         const double t = std::min(hlo + (double)j, (double)kPllTrigStick);
+        // form 23 (the stuck trigOffset, 2^24): the three-candidate runner's stick form (pll_stick)
+        const bool stick = kn.stick != 0;
         const int form = t < 262144.0 ? 17 : t < 524288.0 ? 18 : t < (double)kPllPipeMinLow ? 19
-                       : t < (double)kPllPipeMin5 ? 20 : t < (double)kPllPipeMin ? 21 : 22;
+                       : t < (double)kPllPipeMin5 ? 20 : t < (double)kPllPipeMin ? 21
+                       : (!stick || t < (double)kPllTrigStick) ? 22 : 23;
         const double edge = form == 17 ? 262144.0 : form == 18 ? 524288.0 : form == 19 ? (double)kPllPipeMinLow
-                          : form == 20 ? (double)kPllPipeMin5 : form == 21 ? (double)kPllPipeMin : 0.0;
-        const size_t e = form == 22 ? (size_t)n : std::min((size_t)(edge - hlo), (size_t)n);
+                          : form == 20 ? (double)kPllPipeMin5 : form == 21 ? (double)kPllPipeMin
+                          : form == 22 && stick ? (double)kPllTrigStick : 0.0;
+        const size_t e = edge == 0.0 ? (size_t)n : std::min((size_t)(edge - hlo), (size_t)n);
         const bool cnt = form < 22 && ((kn.cnt >> (form - 17)) & 1) && kPllIdxSimds * n_streams <= n_simd;
         const int kind = cnt ? kStCnt17 + (form - 17)
                        : form == 17 ? kStIdx17 : form == 18 ? kStIdx18 : form == 19 ? kStIdx19
-                       : form == 20 ? kStPipe20 : form == 21 ? kStPipe21 : kStPipe22;
+                       : form == 20 ? kStPipe20 : form == 21 ? kStPipe21 : form == 22 ? kStPipe22 : kStStick;
         timed(kind, (double)(e - j), [&] {
             if (cnt)
                 idx_rc |= launch_pll_cnt(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j,

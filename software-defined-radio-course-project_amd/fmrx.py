@@ -96,13 +96,13 @@ PROTOTYPES = {
 # fmrx_debug_stage_timing's stage kinds (csrc/fmrx_internal.h StageKind)
 STAGES = ["front_end", "bandpass_pair", "pll_prep", "runner_lane", "runner_pred", "runner_sat", "runner_pipe20",
           "runner_pipe21", "runner_pipe22", "pll_check", "pll_tail", "pll_nco", "audio", "runner_idx17", "runner_idx18",
-          "runner_idx19", "runner_cnt17", "runner_cnt18", "runner_cnt19", "runner_cnt20", "runner_cnt21"]
+          "runner_idx19", "runner_cnt17", "runner_cnt18", "runner_cnt19", "runner_cnt20", "runner_cnt21", "runner_stick"]
 
 # fmrx_debug_set_knob's knobs (include/fmrx.h FMRX_KNOB_*): none changes the output; the
 # pll_inject / pll_pipe_miss / pll_hint_skew test hooks make the PLL runners redo work
 KNOBS = {"pll_spec": 0, "pll_sat": 1, "pll_pred": 2, "pll_pipe": 3, "pll_idx": 4, "stereo_chunks": 5,
          "mono_split": 6, "bpf_tile": 7, "halo_kernel": 8, "pll_inject": 9, "pll_pipe_miss": 10,
-         "pll_hint_skew": 11, "pll_cnt": 12}
+         "pll_hint_skew": 11, "pll_cnt": 12, "pll_stick": 13, "stereo_head": 14}
 # knobs every new Receiver applies after fmrx_create (tests set it per test, e.g. with
 # monkeypatch.setattr; the library itself reads only the tuning knobs' environment variables)
 DEFAULT_KNOBS: dict = {}

@@ -842,14 +842,18 @@ def test_pll_predicted_runner(fmrx, orc, monkeypatch, trig0, inject, pred, pipe)
 
 @pytest.mark.parametrize("trig0", [1048600.0, 2097185.0, 4194321.0, 16772216.0, 16777216.0])
 @pytest.mark.parametrize("miss", ["1", "2", "150", "311", "312", "1248", "5000"])
-def test_pll_pipe_redo(fmrx, orc, monkeypatch, trig0, miss):
+@pytest.mark.parametrize("stick", [1, 0])
+def test_pll_pipe_redo(fmrx, orc, monkeypatch, trig0, miss, stick):
     """The three-wave runner's miss path (pll_pipe_kernel): knob pll_pipe_miss=k makes its check
     report interval k as missed (past the last interval: the last), so the chain redoes that
     interval and the two after it exactly and the evaluators restart from the corrected phase.
     20,000 steps = batch 0 + 312 intervals of 64 steps + 1 batch from 2^21 (k = 1, 150, 311 and
     312: the first, a middle one and the verdicts read after the loop), batch 0 + 1,249 intervals
-    of 16 steps in [2^20, 2^21) (1,248 and 1,249 the last two).  Bit-exact, every batch verifies."""
-    knobs(monkeypatch, fmrx, pll_pipe_miss=float(miss))
+    of 16 steps in [2^20, 2^21) (1,248 and 1,249 the last two).  From the stuck trigOffset 2^24
+    (and 5,000 steps before it: the handover inside the call) the stick form (knob pll_stick = 1:
+    the interval's two thresholds once, three e a step) or the plain three-candidate form (0).
+    Bit-exact, every batch verifies."""
+    knobs(monkeypatch, fmrx, pll_pipe_miss=float(miss), pll_stick=stick)
     n = 20000
     rng = np.random.default_rng(int(trig0) % 977)
     t = np.arange(n)
@@ -868,7 +872,8 @@ def test_pll_pipe_redo(fmrx, orc, monkeypatch, trig0, miss):
         assert same(buf.cpu().numpy(), want_x)
         assert same(st.cpu().numpy(), want_st)
         resumed, checked = counts.cpu().tolist()
-        assert checked == n // 16 and resumed == 0, (resumed, checked)
+        # each launch counts its whole batches: a range split at a form's edge (the stick) loses one
+        assert n // 16 - 1 <= checked <= n // 16 and resumed == 0, (resumed, checked)
 
 
 @pytest.mark.parametrize("trig0", [131072.0, 262177.0, 524188.0, 600000.0, 1043576.0, 125000.0])

@@ -15,6 +15,7 @@
 #   n2        the N=2 bench line rehearsed with gloo (both ranks on device 0), chunked configs[4] gather
 #   profmono  tools/gpu_bench_prof.sh (bench line, kernel trace, FETCH/WRITE/GRBM passes of the fused kernel)
 #   libab     stage_times per library in $LIBS (A/B builds), alternating, twice
+#   rec       the record: tests smoke, tools/gpu_bench_prof.sh (bench line, trace, PMC), mode2 stages seam
 #   smoke     __graft_entry__.smoke()
 set -o pipefail
 TAG=${1:-r05}; shift
@@ -75,6 +76,10 @@ for step in "$@"; do
              > $OUT/libab_${r}_$tagl.json 2>> $OUT/libab.err || { tail $OUT/libab.err; exit 16; }
            echo "$r $lib $(python tools/stage_summary.py $OUT/libab_${r}_$tagl.json)"
          done; done ;;
+    rec) # the round's record at HEAD: GPU suite, smoke, bench line + kernel trace + PMC passes of the
+         # fused kernel (tools/gpu_bench_prof.sh), configs[3]'s passes, stage times, the seam
+         bash tools/gpu_r05.sh $TAG tests smoke && bash tools/gpu_bench_prof.sh $TAG/prof_mono && \
+         bash tools/gpu_r05.sh $TAG mode2 stages seam || exit 21 ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail $OUT/smoke.log; exit 5; }
            tail -1 $OUT/smoke.log ;;
   esac
