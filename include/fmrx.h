@@ -60,9 +60,11 @@ typedef struct {
                      /* limit; fmrx_create refuses more with FMRX_EINVAL).  Device memory per   */
                      /* stream: 2 halos (~26 KiB) + the audio history; stereo adds the demod /  */
                      /* channel / carrier rows (3 x 4 B per IF sample of a call) and the PLL    */
-                     /* scratch, ~32.5 B per sample of a segment (2^18 samples per stream, fewer */
+                     /* scratch: ~32.5 B per sample of a segment (2^18 samples per stream, fewer */
                      /* past 32 streams: segment x streams ~2^23, >= 2^14 -- ~0.5 MB a stream at */
-                     /* 2,048 streams).                                                           */
+                     /* 2,048 streams) plus the call's trigArgs, 4 B per IF sample of a call (the */
+                     /* NCO reads them after the runners; one 1 GiB mode-0 call: ~200 MB; the    */
+                     /* pipelined engine from 16 streams holds two such side buffers).           */
     int device;      /* HIP device ordinal                                                     */
 } fmrx_config;
 

@@ -60,15 +60,6 @@ __device__ unsigned int g_redo_stream[4][kProfStreams];
 #define PROF_T() 0ull
 #endif
 
-
-// A/B build only (AB=-DFMRX_AB_V256): the CU-a-stream runners (index, count) take 256 VGPRs a wave,
-// so a SIMD holds two of their waves and a CU one five-wave workgroup: two streams' chains can
-// then not be placed on one CU
-#ifdef FMRX_AB_V256
-#define FMRX_ONE_WG_A_CU() asm volatile("" ::: "v255")
-#else
-#define FMRX_ONE_WG_A_CU() (void)0
-#endif
 namespace {
 
 // e of a step (input v, 1/v = iv, half turn h = 0.5 [v < 0]) whose previous trigArg is a:
@@ -1133,7 +1124,6 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
                float* out_base, size_t ostride, int inject, int miss, float lo, float hi, unsigned long long* stats,
                unsigned* redos) {
     constexpr int NI = 16;          // steps an interval
-    FMRX_ONE_WG_A_CU();
     constexpr int SPP = 64 / NC;    // steps a candidate row
     constexpr int NR = NI / SPP;    // candidate rows an interval
     constexpr int HC = NC / 2;      // candidates c0 - HC .. c0 + HC - 1
@@ -1437,7 +1427,6 @@ __global__ void __launch_bounds__(64 * (1 + NW)) __attribute__((amdgpu_waves_per
 pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step, float norm_bw, float* st,
                float* out_base, size_t ostride, int inject, int miss, float lo, float hi, unsigned long long* stats,
                unsigned* redos) {
-    FMRX_ONE_WG_A_CU();
     constexpr int NP = NC + 2;  // row slots: T(c_base + l) l <= NC, +inf | NaN, e(c_base + l - 1), NaN
     constexpr int HC = NC / 2;  // candidates c0 - HC .. c0 + HC
     constexpr int RD = 4;       // intervals of step inputs in flight

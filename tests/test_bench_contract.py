@@ -48,16 +48,22 @@ def test_bench_json_contract():
     # against the serial chain's instruction floor per PLL regime
     r3 = oc["configs[3]"]["roofline"]
     assert 0 < r3["frac"] < 1 and 0 < r3["binding"]["frac"] < 1 and r3["kernel_ms"] > 0
+    # its PMC traffic only with the stamp of the kernel sources that ran (profiles/traffic_mode2.json)
+    assert r3.get("traffic") is None or (r3["traffic_source"] and 1.0 <= r3["traffic_over_alg"] < 1.1), r3
     for c in ("configs[2]", "configs[4]"):
         lat = oc[c]["latency"]
         assert lat["runner_ms"] > 0 and lat["regimes"], lat
         for k, r in lat["regimes"].items():
             assert k.startswith("runner_") and 0 < r["frac"] <= 1.0 and r["ns_per_step"] > r["floor_ns_per_step"], (k, r)
+            # and against the chain's measured dependent latency (tools/ubench_cnt.hip)
+            assert r["latency_floor_ns_per_step"] >= r["floor_ns_per_step"] and 0 < r["frac_of_latency_floor"] <= 1.0, (k, r)
     # configs[4] (256 stereo streams; 0.5 s each here, 60 s by default) checked against the
     # reference build's per-stream hashes
     c4 = oc["configs[4]"]
     assert "error" not in c4, c4
     assert c4["n_gpus"] == 1 and c4["checked_streams"] == [0, 7, 8, 15] and c4["bit_exact_vs_reference"] is True
+    # the self-certifying runners' redone intervals per stream, from the untimed warm-up call
+    assert c4["redos"]["streams"] == 256 and len(c4["redos"]["worst_streams"]) == 8, c4.get("redos")
     # each rank's own split (one rank here) and the process group it ran in
     assert c4["dist"]["world_size"] == 1 and len(c4["per_rank"]) == 1 and c4["per_rank"][0]["streams"] == 256
     rf = j["roofline"]

@@ -1014,6 +1014,39 @@ def test_index_runner_streams(fmrx, monkeypatch):
     assert np.array_equal(outs[0], outs[2]) and np.array_equal(outs[1], outs[2])
 
 
+def test_count_runner_streams(fmrx, monkeypatch):
+    """pll_cnt_kernel over many streams (200: a CU each still fits), every stream put at trigOffset
+    2^20 - 10,000 through the state blob (the [2^19, 2^20) form hands over to the [2^20, 2^21) one
+    inside the call), 24 blocks in one call: the PCM equals the same call with the count runner off
+    (knob pll_cnt = 0: the index runner and the three-wave runner's 16-step form), and no batch is
+    redone on the inject hook's account."""
+    ns, nb, bb = 200, 24, 12800
+    ins = np.stack([iqgen.make("synth:%d" % (740 + s % 5), (nb + 2) * bb) for s in range(ns)])
+    outs = []
+    for cnt in (12, 0):
+        knobs(monkeypatch, fmrx, pll_cnt=cnt)
+        with fmrx.Receiver(0, fmrx.STEREO, n_streams=ns) as rx:
+            rx.process(ins[:, : 2 * bb])
+            blob = bytearray(rx.get_state())
+            hdr = np.frombuffer(bytes(blob[:40]), np.uint32)
+            pll_off = 40 + ns * (int(hdr[6]) + 4 * int(hdr[7]) + 4 * 64)
+            pll = np.frombuffer(bytes(blob[pll_off: pll_off + ns * 32]), np.float32).reshape(ns, 8).copy()
+            pll[:, 5] = 1048576.0 - 10000.0
+            blob[pll_off: pll_off + ns * 32] = pll.tobytes()
+            rx.set_state(bytes(blob))
+            counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+            redos = torch.zeros((ns, 4), dtype=torch.int32, device="cuda")
+            rx.debug_pll_stats(counts.data_ptr())
+            rx.debug_pll_redos(redos.data_ptr())
+            outs.append(rx.process(ins[:, 2 * bb:]))
+            rx.debug_pll_stats(None)
+            rx.debug_pll_redos(None)
+        resumed, checked = counts.cpu().tolist()
+        assert checked > 0 and resumed == 0, (cnt, resumed, checked)
+        assert int(redos.sum()) >= 0
+    assert np.array_equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("mixed", [False, True])
 def test_pipe_runner_streams(fmrx, monkeypatch, mixed):
     """pll_pipe_kernel over many streams (300: three waves each still fit the SIMDs), every
