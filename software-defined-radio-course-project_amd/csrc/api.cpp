@@ -135,6 +135,7 @@ struct fmrx_ctx {
         PllKnobs pll;
         int stereo_chunks = 0;  // 0: by stream count and call length; k: k chunks (1: serial engine)
         int stereo_head = 8;    // the first chunk's blocks in 16ths of a middle chunk's
+        int stereo_lead = 0;    // n > 0: chunk k's front end waits for chunk k - n's PLL; 0: none
         int mono_split = -1;    // -1: kOlderShare; 0: equal spans; n: the older wave's n / 1024
         int bpf_tile = 1;       // 0: the per-output band-pass kernel
         int halo_kernel = 0;    // 1: the separate halo_kernel after the fused one
@@ -620,6 +621,9 @@ int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks,
         const size_t nb = b1 - b0, m = nb * ipb, off = b0 * ipb;
         const bool last = k == K - 1;
         if (k == 1 && lane_m > 0) HIPCHK(hipStreamWaitEvent(c->s_front, ev_lane, 0));
+        // paced: chunk k's front end runs beside chunk k - lead + 1's PLL, not all of them at the start
+        const int lead = c->knobs.stereo_lead;
+        if (lead > 0 && k >= lead) HIPCHK(hipStreamWaitEvent(c->s_front, ev_pll(k - lead), 0));
         // s_front: front end and band-pass pair of chunk k
         if ((rc = run_fused(c, d_iq, nb, nullptr, nullptr, c->d_demod.p, c->demod_stride, kDemodHist, false, b0,
                             n_blocks, c->s_front, last)))
@@ -764,6 +768,7 @@ static fmrx_ctx::Knobs knobs_from_env() {
     k.pll.stick = get("FMRX_PLL_STICK", 1);
     k.stereo_chunks = std::max(0, get("FMRX_STEREO_CHUNKS", 0));
     k.stereo_head = std::max(1, get("FMRX_STEREO_HEAD", 8));
+    k.stereo_lead = std::max(0, get("FMRX_STEREO_LEAD", 0));
     k.mono_split = get("FMRX_MONO_SPLIT", -1);
     k.bpf_tile = get("FMRX_BPF_TILE", 1);
     k.halo_kernel = get("FMRX_HALO_KERNEL", 0);
@@ -1469,6 +1474,7 @@ int fmrx_debug_set_knob(fmrx_ctx* c, int knob, double value) {
         case FMRX_KNOB_PLL_IDX: k.pll.idx = v; break;
         case FMRX_KNOB_STEREO_CHUNKS: k.stereo_chunks = std::max(0, v); break;
         case FMRX_KNOB_STEREO_HEAD: k.stereo_head = std::max(1, v); break;
+        case FMRX_KNOB_STEREO_LEAD: k.stereo_lead = std::max(0, v); break;
         case FMRX_KNOB_MONO_SPLIT: k.mono_split = v; break;
         case FMRX_KNOB_BPF_TILE: k.bpf_tile = v; break;
         case FMRX_KNOB_HALO_KERNEL: k.halo_kernel = v; break;

@@ -579,6 +579,11 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                                                       unsigned long long* stats, unsigned* redos) {
     constexpr int NI = NB * BPI;
     static_assert(NI == 16 || NI == 32 || NI == 64, "the evaluators' lane map: 64 / NI lanes a step");
+#ifdef FMRX_AB_PIPE_EXCL
+    // A/B build only: each wave claims its SIMD's whole register file, so no stage-kernel wave
+    // shares a chain's (or an evaluator's) SIMD; the fourth SIMD of the CU stays open
+    asm volatile("" ::: "a255");
+#endif
     static_assert(NC == 3 || NC == 5, "three or five candidates");
     // STK: the stuck trigOffset (2^24, filter.cpp:165-166: 69.9 s into a stream).  Every step's
     // P is then the same, so c0 = float(P + phase_ref) and the two thresholds are the interval's

@@ -486,17 +486,21 @@ def test_stereo_multistream(fmrx, orc):
         assert np.array_equal(out[s], orc.run(0, 51, iq, ["pcm"])["pcm"]), s
 
 
-@pytest.mark.parametrize("mode,n_streams,nb,chunks", [(0, 5, 48, "3"), (0, 1, 64, "4"), (1, 3, 40, "2"),
-                                                      (2, 2, 3, "2"), (0, 70, 120, None)])
-def test_stereo_pipelined_chunks(fmrx, orc, monkeypatch, mode, n_streams, nb, chunks):
+@pytest.mark.parametrize("mode,n_streams,nb,chunks,lead", [(0, 5, 48, "3", 0), (0, 1, 64, "4", 0), (1, 3, 40, "2", 0),
+                                                           (2, 2, 3, "2", 0), (0, 70, 120, None, 0),
+                                                           (0, 5, 48, "4", 1), (0, 70, 120, None, 2)])
+def test_stereo_pipelined_chunks(fmrx, orc, monkeypatch, mode, n_streams, nb, chunks, lead):
     """The pipelined stereo engine (api.cpp run_stereo_pipelined): a call's blocks in chunks,
     front end + band-pass of chunk k + 1 and audio of chunk k - 1 on their own HIP streams beside
     the PLL of chunk k, every chunk reading the call's buffers at its offset (a chunk's RF halo
     is the call's own bytes in front of it).  knob stereo_chunks forces the chunk count (None: the
     default, 8 from 16 streams, fewer when a chunk would hold < 2^14 samples); two calls in a row
-    check the carried state.  Modes 0/1 take the tiled audio kernel, mode 2 the per-frame one."""
+    check the carried state.  Modes 0/1 take the tiled audio kernel, mode 2 the per-frame one.
+    lead > 0: the paced schedule (chunk k's front end after chunk k - lead's PLL)."""
+    kw = {"stereo_lead": float(lead)}
     if chunks is not None:
-        knobs(monkeypatch, fmrx, stereo_chunks=float(chunks))
+        kw["stereo_chunks"] = float(chunks)
+    knobs(monkeypatch, fmrx, **kw)
     bb = oracle.MODES[mode][0]
     rf_fs = oracle.MODES[mode][3]
     recipes = [("synth:%d" if s % 3 else "rand:%d") % (500 + s) for s in range(n_streams)]

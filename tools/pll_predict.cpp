@@ -140,12 +140,13 @@ int main(int argc, char** argv) {
     // moves by about integ a step, filter.cpp:161-162), s the step of the reference state; the
     // fraction of B-step batches whose every step is within m floats of that centre
     std::printf("B-step batches within m floats of the extrapolated centre, lookback %d:\n", lb);
-    std::printf("%-22s %s\n", "j range", "m = 0 1 2 3 4");
-    for (int B : {16, 64})
+    const int mx[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 12, 16};
+    std::printf("%-22s %s\n", "j range", "m = 0 1 2 3 4 5 6 7 8 12 16");
+    for (int B : {16, 32, 64})
     for (int e = 17; e < 25; e++) {
         const size_t j0 = (size_t)1 << e, j1 = std::min(e == 24 ? N : ((size_t)1 << (e + 1)), N);
         if (j0 >= j1) continue;
-        long nb_all = 0, ok[5] = {}, okc[5] = {};
+        long nb_all = 0, ok[11] = {}, okc[11] = {};
         for (size_t b0 = j0; b0 + B <= j1; b0 += B) {
             const size_t back = (size_t)(lb - 1) * B + 1;
             const size_t sref = b0 - back;
@@ -159,15 +160,15 @@ int main(int argc, char** argv) {
                 kmaxc = std::max(kmaxc, std::labs(ulps_between(cand0, arg[j])));
             }
             nb_all++;
-            for (int q = 0; q < 5; q++) {
-                ok[q] += kmax <= q;
-                okc[q] += kmaxc <= q;
+            for (int q = 0; q < 11; q++) {
+                ok[q] += kmax <= mx[q];
+                okc[q] += kmaxc <= mx[q];
             }
         }
         std::printf("[2^%d, 2^%d)  B=%-3d extrap", e, e + 1, B);
-        for (int q = 0; q < 5; q++) std::printf(" %.5f", (double)ok[q] / nb_all);
-        std::printf("   plain");
-        for (int q = 0; q < 5; q++) std::printf(" %.5f", (double)okc[q] / nb_all);
+        for (int q = 0; q < 11; q++) std::printf(" %.4f", (double)ok[q] / nb_all);
+        std::printf("\n                    plain ");
+        for (int q = 0; q < 11; q++) std::printf(" %.4f", (double)okc[q] / nb_all);
         std::printf("\n");
     }
     // below 2^22: fraction of B-step batches whose every step is within m floats of c0 (2m + 1
