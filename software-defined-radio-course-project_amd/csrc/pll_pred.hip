@@ -48,7 +48,7 @@ namespace fmrx {
 // barrier wait, summed over every batch and workgroup, printed at exit
 __device__ unsigned long long g_pred_prof[6];
 __device__ unsigned long long g_pipe_prof[6];
-__device__ unsigned long long g_pipe_prof_w2[2];  // wave 2's body / barrier wait
+__device__ unsigned long long g_pipe_prof_w2[4];  // wave 2's body / barrier wait / put / check
 __device__ unsigned long long g_miss_reason[3];   // pll_pipe_kernel's missed steps by reason
 __device__ unsigned long long g_idx_prof[6];
 __device__ unsigned long long g_cnt_prof[6];
@@ -579,11 +579,6 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                                                       unsigned long long* stats, unsigned* redos) {
     constexpr int NI = NB * BPI;
     static_assert(NI == 16 || NI == 32 || NI == 64, "the evaluators' lane map: 64 / NI lanes a step");
-#ifdef FMRX_AB_PIPE_EXCL
-    // A/B build only: each wave claims its SIMD's whole register file, so no stage-kernel wave
-    // shares a chain's (or an evaluator's) SIMD; the fourth SIMD of the CU stays open
-    asm volatile("" ::: "a255");
-#endif
     static_assert(NC == 3 || NC == 5, "three or five candidates");
     // STK: the stuck trigOffset (2^24, filter.cpp:165-166: 69.9 s into a stream).  Every step's
     // P is then the same, so c0 = float(P + phase_ref) and the two thresholds are the interval's
@@ -616,7 +611,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     constexpr bool REPLAY = BPI > 1;
     __shared__ float sph[REPLAY ? 1 : 4][REPLAY ? 1 : NI];
     __shared__ int smiss[4], sexact[4];
-    __shared__ float sek[STK ? 4 : 1][STK ? 3 * NI : 4];
+    __shared__ __attribute__((aligned(16))) float sek[STK ? 4 : 1][STK ? 3 * NI : 4];
     __shared__ float2 sthr[4];
     // the candidate data the chain and the replay select from at step J of ring slot sl: (T0, T1,
     // e(c0 - 1), e(c0)) and e(c0 + 1)
@@ -718,11 +713,13 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                     else if (NC == 3) reinterpret_cast<float*>(&sel[sl][l])[2 + r] = e;
                     else reinterpret_cast<float*>(&sel2[NC == 5 ? sl : 0][NC == 5 ? l : 0])[r] = e;
                 }
+                // the stick form's two thresholds, the interval's constants (every step's P and c0
+                // are the same): here, where the evaluations leave time, not in wave 2 -- its check
+                // sets the stick form's pace (profiles/r05/rprof_w2/)
+                if (STK && t == 0)
+                    sthr[sl] = make_float2(phase_thr(pr, cb + (uint32_t)(1 - HC)), phase_thr(pr, cb + (uint32_t)(2 - HC)));
             } else {
-                if (STK) {  // the interval's two thresholds (every step's P and c0 are the same)
-                    if (h == 0 && l == 0)
-                        sthr[sl] = make_float2(phase_thr(pr, cb + (uint32_t)(1 - HC)), phase_thr(pr, cb + (uint32_t)(2 - HC)));
-                } else {
+                if (!STK) {
                     for (int r = h; r < NC - 1; r += LPS)
                         reinterpret_cast<float*>(&sel[sl][l])[r] = phase_thr(pr, cb + (uint32_t)(r + 1 - HC));
                 }
@@ -804,11 +801,25 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             // LDS); lane l keeps the phase of step l and checks its own trigArg afterwards
             float4 da[NB], da2[NC == 5 ? NB : 1];
             float dep[NB];
+            if constexpr (STK) {  // the batch's three e a step as 16-byte reads, the thresholds once
+                const float2 T = sthr[sl];
+                float ek[3 * NB];
 #pragma unroll
-            for (int j = 0; j < NB - 1; j++) {
-                da[j] = cand(sl, NB * gb + j);
-                dep[j] = cand_ep(sl, NB * gb + j);
-                if constexpr (NC == 5) da2[j] = sel2[NC == 5 ? sl : 0][NC == 5 ? NB * gb + j : 0];
+                for (int q = 0; q < 3 * NB / 4; q++)
+                    *reinterpret_cast<float4*>(&ek[4 * q]) =
+                        reinterpret_cast<const float4*>(&sek[STK ? sl : 0][STK ? 3 * NB * gb : 0])[q];
+#pragma unroll
+                for (int j = 0; j < NB - 1; j++) {
+                    da[j] = make_float4(T.x, T.y, ek[3 * j], ek[3 * j + 1]);
+                    dep[j] = ek[3 * j + 2];
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < NB - 1; j++) {
+                    da[j] = cand(sl, NB * gb + j);
+                    dep[j] = cand_ep(sl, NB * gb + j);
+                    if constexpr (NC == 5) da2[j] = sel2[NC == 5 ? sl : 0][NC == 5 ? NB * gb + j : 0];
+                }
             }
             // pll_batch_fast's range test, on the state at the batch's start
             const bool range_ok = fabsf(r0.y) < kPllMaxPhase && fabsf(r0.x) < kPllMaxInteg;
@@ -836,7 +847,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         put(1, p.phase, vq[1 % RD]);  // interval 1 from the initial phase
         ld(1 + RD, vq[1 % RD]);
         __syncthreads();  // (prologue)
-        unsigned long long ev_body = 0, ev_wait = 0;
+        unsigned long long ev_body = 0, ev_wait = 0, ev_put = 0, ev_check = 0;
         // interval i: interval i + 1's data, interval i - 1's check; groups of RD intervals from
         // i0 = 1 (mod RD), so the ring slots are compile-time
         for (int i0 = 1; i0 <= ni; i0 += RD) {
@@ -851,7 +862,10 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                             put(i + 1, sst[(i - 1) & 3][BPI - 1].y, vq[sl]);
                             ld(i + 1 + RD, vq[sl]);
                         }
+                        const unsigned long long pa = PROF_T();
                         check(i - 1);
+                        ev_put += pa - p0;
+                        ev_check += PROF_T() - pa;
                         const int redo = __builtin_amdgcn_readfirstlane(smiss[(i - 2) & 3]);
                         if (redo) {
                             // the chain redoes interval i - 2 exactly, then runs i - 1 again on
@@ -891,10 +905,14 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         if (t == 0 && w == 2) {
             atomicAdd(&g_pipe_prof_w2[0], ev_body);
             atomicAdd(&g_pipe_prof_w2[1], ev_wait);
+            atomicAdd(&g_pipe_prof_w2[2], ev_put);
+            atomicAdd(&g_pipe_prof_w2[3], ev_check);
         }
 #endif
         (void)ev_body;
         (void)ev_wait;
+        (void)ev_put;
+        (void)ev_check;
         return;
     }
 
@@ -1744,11 +1762,12 @@ static void print_pred_prof() {
     if (hipMemcpyFromSymbol(mr, HIP_SYMBOL(g_miss_reason), sizeof mr) == hipSuccess && (mr[0] | mr[1] | mr[2]))
         std::fprintf(stderr, "pll_pipe missed steps: trigArg outside the candidates %llu, e uncertified %llu, "
                      "threshold outside its window %llu\n", mr[0], mr[1], mr[2]);
-    unsigned long long h2[2] = {};
+    unsigned long long h2[4] = {};
     (void)hipMemcpyFromSymbol(h2, HIP_SYMBOL(g_pipe_prof_w2), sizeof h2);
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pipe_prof), sizeof h) == hipSuccess && h[4])
-        std::fprintf(stderr, "pll_pipe prof: wave 2 body %.1f wait %.1f (shader cycles per interval)\n",
-                     (double)h2[0] / h[4], (double)h2[1] / h[4]);
+        std::fprintf(stderr, "pll_pipe prof: wave 2 body %.1f wait %.1f, of the body its data %.1f and its check %.1f "
+                     "(shader cycles per interval)\n", (double)h2[0] / h[4], (double)h2[1] / h[4], (double)h2[2] / h[4],
+                     (double)h2[3] / h[4]);
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pipe_prof), sizeof h) == hipSuccess && h[4])
         std::fprintf(stderr, "pll_pipe prof: intervals %llu chain body %.1f wait %.1f, evaluator body %.1f wait %.1f "
                      "(shader cycles per interval), %llu redos\n", h[4], (double)h[0] / h[4], (double)h[1] / h[4],
