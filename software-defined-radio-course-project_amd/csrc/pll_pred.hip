@@ -1871,6 +1871,9 @@ static int cnt_launch(hipStream_t s, const float* io, int n, int n_streams, size
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+#ifndef FMRX_CNT_NW
+#define FMRX_CNT_NW 4  // evaluator waves of the [2^19, 2^21) count forms
+#endif
 int launch_pll_cnt(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
                    float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats,
                    unsigned* redos) {
@@ -1886,10 +1889,10 @@ int launch_pll_cnt(hipStream_t s, const float* io, int n, int n_streams, size_t 
             return cnt_launch<16, 31, 4>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
                                          262144.0f, 524287.0f, stats, redos);
         case 19:
-            return cnt_launch<32, 15, 4>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
+            return cnt_launch<32, 15, FMRX_CNT_NW>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
                                          524288.0f, 1048575.0f, stats, redos);
         case 20:
-            return cnt_launch<64, 15, 4>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
+            return cnt_launch<64, 15, FMRX_CNT_NW>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
                                          kPllPipeMinLow, kPllPipeMin5 - 1.0f, stats, redos);
         default:  // three waves a stream, as the three-wave runner it would replace
             return cnt_launch<64, 7, 2>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
