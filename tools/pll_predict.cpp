@@ -171,6 +171,26 @@ int main(int argc, char** argv) {
         for (int q = 0; q < 11; q++) std::printf(" %.4f", (double)okc[q] / nb_all);
         std::printf("\n");
     }
+    // past the stick (trigOffset 2^24: one constant P, trigArg on a 1-rad grid): the fraction of
+    // B-step batches whose trigArgs are all one float (one candidate for the whole batch), and the
+    // mean run of one trigArg
+    if (N > (1u << 24) + 4096) {
+        std::printf("past the stick: B-step batches with one trigArg throughout\n");
+        for (int B : {8, 16, 32, 64, 128, 256}) {
+            long nb_all = 0, one = 0;
+            for (size_t b0 = (size_t)1 << 24; b0 + B <= N; b0 += B) {
+                bool same = true;
+                for (size_t j = b0 + 1; j < b0 + B; j++) same = same && arg[j] == arg[b0];
+                nb_all++;
+                one += same;
+            }
+            std::printf("  B=%-4d %.4f of %ld\n", B, (double)one / nb_all, nb_all);
+        }
+        long runs = 0;
+        for (size_t j = ((size_t)1 << 24) + 1; j < N; j++) runs += arg[j] != arg[j - 1];
+        std::printf("  trigArg changes %ld in %zu steps: mean run %.1f steps\n", runs, N - ((size_t)1 << 24),
+                    (double)(N - ((size_t)1 << 24)) / (double)(runs + 1));
+    }
     // below 2^22: fraction of B-step batches whose every step is within m floats of c0 (2m + 1
     // candidates), per octave of j -- how many candidates a chain would need there
     const int ms[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 31};
