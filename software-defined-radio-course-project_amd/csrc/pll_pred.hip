@@ -1785,6 +1785,9 @@ void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_str
                        seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, sat_ok, pipe_on);
 }
 
+#ifndef FMRX_PIPE_RD
+#define FMRX_PIPE_RD 8  // intervals of step inputs in flight (the evaluators' loop is unrolled by it)
+#endif
 void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
                      float* st, float* out, size_t ostride, int inject, int miss, int form,
                      unsigned long long* stats, unsigned* redos) {
@@ -1793,16 +1796,16 @@ void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_
 #endif
     if (n <= 0) return;
     if (form == 23)
-        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8, 3, true>), dim3(n_streams), dim3(192), 0, s, io, n,
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, FMRX_PIPE_RD, 3, true>), dim3(n_streams), dim3(192), 0, s, io, n,
                            n_streams, stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
     else if (form == 22)
-        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8, 3>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, FMRX_PIPE_RD, 3>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
                            stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
     else if (form == 21)
-        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, 8, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, FMRX_PIPE_RD, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
                            stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
     else
-        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 1, 8, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 1, FMRX_PIPE_RD, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
                            stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
 }
 
