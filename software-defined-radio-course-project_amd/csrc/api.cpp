@@ -136,6 +136,7 @@ struct fmrx_ctx {
         int stereo_chunks = 0;  // 0: by stream count and call length; k: k chunks (1: serial engine)
         int stereo_head = 8;    // the first chunk's blocks in 16ths of a middle chunk's
         int stereo_lead = 0;    // n > 0: chunk k's front end waits for chunk k - n's PLL; 0: none
+        int audio_defer = 1;    // every chunk's audio stage after the last chunk's PLL (its NCO not); 0: beside
         int mono_split = -1;    // -1: kOlderShare; 0: equal spans; n: the older wave's n / 1024
         int bpf_tile = 1;       // 0: the per-output band-pass kernel
         int halo_kernel = 0;    // 1: the separate halo_kernel after the fused one
@@ -659,10 +660,25 @@ int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks,
             return fail(FMRX_EHIP, "NCO launch failed");
         c->stage_timer.end(t_nco, kStNco, 0.0, c->s_audio);
         HIPCHK(hipEventRecord(ev_nco(k), c->s_audio));
-        const int t_au = c->stage_timer.begin(c->s_audio);
-        if (launch_stereo_audio_range(A, (int)b0, (int)b1, last, ns, c->s_audio))
-            return fail(FMRX_EHIP, "stereo audio launch failed");
-        c->stage_timer.end(t_au, kStAudio, 0.0, c->s_audio);
+        // (audio_defer, the default: the audio stages after the loop -- their LDS tiles then never
+        // run beside a PLL chain, whose LDS reads they slow (tools/ubench_noise.hip); configs[4]
+        // 0.4168 -> 0.4113 s, profiles/r05/ab_audio_defer/)
+        if (!c->knobs.audio_defer) {
+            const int t_au = c->stage_timer.begin(c->s_audio);
+            if (launch_stereo_audio_range(A, (int)b0, (int)b1, last, ns, c->s_audio))
+                return fail(FMRX_EHIP, "stereo audio launch failed");
+            c->stage_timer.end(t_au, kStAudio, 0.0, c->s_audio);
+        }
+    }
+    if (c->knobs.audio_defer) {
+        for (int k = 0; k < K; k++) {
+            const int t_au = c->stage_timer.begin(c->s_audio);
+            if (launch_stereo_audio_range(A, (int)chunk_begin(n_blocks, k, K, c->knobs.stereo_head),
+                                          (int)chunk_begin(n_blocks, k + 1, K, c->knobs.stereo_head), k == K - 1, ns,
+                                          c->s_audio))
+                return fail(FMRX_EHIP, "stereo audio launch failed");
+            c->stage_timer.end(t_au, kStAudio, 0.0, c->s_audio);
+        }
     }
     // demod history for the next call (after every read of this call's demod: the last audio
     // launch follows every band-pass launch through the events)
@@ -769,6 +785,7 @@ static fmrx_ctx::Knobs knobs_from_env() {
     k.stereo_chunks = std::max(0, get("FMRX_STEREO_CHUNKS", 0));
     k.stereo_head = std::max(1, get("FMRX_STEREO_HEAD", 8));
     k.stereo_lead = std::max(0, get("FMRX_STEREO_LEAD", 0));
+    k.audio_defer = get("FMRX_AUDIO_DEFER", 1);
     k.mono_split = get("FMRX_MONO_SPLIT", -1);
     k.bpf_tile = get("FMRX_BPF_TILE", 1);
     k.halo_kernel = get("FMRX_HALO_KERNEL", 0);
@@ -1475,6 +1492,7 @@ int fmrx_debug_set_knob(fmrx_ctx* c, int knob, double value) {
         case FMRX_KNOB_STEREO_CHUNKS: k.stereo_chunks = std::max(0, v); break;
         case FMRX_KNOB_STEREO_HEAD: k.stereo_head = std::max(1, v); break;
         case FMRX_KNOB_STEREO_LEAD: k.stereo_lead = std::max(0, v); break;
+        case FMRX_KNOB_AUDIO_DEFER: k.audio_defer = v; break;
         case FMRX_KNOB_MONO_SPLIT: k.mono_split = v; break;
         case FMRX_KNOB_BPF_TILE: k.bpf_tile = v; break;
         case FMRX_KNOB_HALO_KERNEL: k.halo_kernel = v; break;
