@@ -578,14 +578,17 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                                                       size_t ostride, int inject, int miss,
                                                       unsigned long long* stats, unsigned* redos) {
     constexpr int NI = NB * BPI;
-    static_assert(NI == 16 || NI == 32 || NI == 64, "the evaluators' lane map: 64 / NI lanes a step");
+    static_assert(NI == 16 || NI == 32 || NI == 64 || (NC == 3 && NI == 128),
+                  "the evaluators' lane map: 64 / NI lanes a step, or NI / 64 steps a lane");
     static_assert(NC == 3 || NC == 5, "three or five candidates");
     // STK: the stuck trigOffset (2^24, filter.cpp:165-166: 69.9 s into a stream).  Every step's
     // P is then the same, so c0 = float(P + phase_ref) and the two thresholds are the interval's
     // constants: wave 2 forms them once (sthr) and the e of the three candidates sit three floats a
     // step (sek) -- 0.75 16-byte reads a step for the chain instead of 1.25
     static_assert(!STK || (NC == 3 && BPI > 1), "the stick form is the three-candidate replay form");
-    constexpr int LPS = 64 / NI;  // evaluator lanes a step
+    constexpr int NIL = NI > 64 ? 64 : NI;  // the evaluators' lane map: step l + NIL sp on lane l
+    constexpr int SPL = NI / NIL;          // steps a lane (128-step intervals: two)
+    constexpr int LPS = 64 / NIL;          // evaluator lanes a step
     constexpr int HC = NC / 2;    // candidates c0 - HC .. c0 + HC
     // the chain's steps a burst of reads (its registers hold a burst's data)
 #ifndef FMRX_CHM
@@ -628,7 +631,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         else return sep[sl][J];
     };
     // the wave (readfirstlane: uniform, so the waves' branches and loops are scalar)
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63, l = t & (NI - 1), h = t / NI;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63, l = t & (NIL - 1), h = t / NIL;
     const int s = blockIdx.x;  // grid = n_streams
     const float* x = io + (size_t)s * stride;
     float* out = out_base + (size_t)s * ostride;
@@ -684,17 +687,24 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
 
     if (w > 0) {
         // ring of RD intervals of step inputs, interval k in slot k % RD, loaded RD - 1 ahead
-        float vq[RD];
-        auto ld = [&](int k, float& v) {
-            const int j = j0(k <= ni ? k : ni) + l;
-            v = x[min(j + 1, n - 1)];  // the step the e is for
+        float vq[RD][SPL];
+        auto ld = [&](int k, float (&v)[SPL]) {
+#pragma unroll
+            for (int sp = 0; sp < SPL; sp++) {
+                const int j = j0(k <= ni ? k : ni) + l + NIL * sp;
+                v[sp] = x[min(j + 1, n - 1)];  // the step the e is for
+            }
         };
         // interval k's candidate data from phase_ref, the phase at the start of interval k - 1:
         // E1 lane (h, l) the e (and its certification) of candidates c0 - HC + r of step l, r = h,
         // h + LPS, ... < NC; E2 lane (h, l) the thresholds of c0 - HC + 1 + r, r = h, h + LPS,
         // ... < NC - 1, lanes h = 0 also c0's bits and P
-        auto put = [&](int k, float phase_ref, float v) {
-            const int j = j0(k <= ni ? k : ni) + l;
+        auto put = [&](int k, float phase_ref, const float (&vs)[SPL]) {
+#pragma unroll
+          for (int sp = 0; sp < SPL; sp++) {
+            const int ls = l + NIL * sp;  // this lane's step
+            const float v = vs[sp];
+            const int j = j0(k <= ni ? k : ni) + ls;
             const double pr = pr_at(j);
             const float c0 = (float)(pr + (double)phase_ref);
             const uint32_t cb = __builtin_bit_cast(uint32_t, c0);
@@ -707,27 +717,28 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 for (int r = h; r < NC; r += LPS) {
                     bool ok;
                     const float e = pred_e_cert(__builtin_bit_cast(float, cb + (uint32_t)(r - HC)), v, iv, ok);
-                    scert[sl][l][r] = ok ? 1 : 0;
-                    if (STK) sek[STK ? sl : 0][STK ? 3 * l + r : 0] = e;
-                    else if (r == NC - 1) sep[sl][l] = e;
-                    else if (NC == 3) reinterpret_cast<float*>(&sel[sl][l])[2 + r] = e;
-                    else reinterpret_cast<float*>(&sel2[NC == 5 ? sl : 0][NC == 5 ? l : 0])[r] = e;
+                    scert[sl][ls][r] = ok ? 1 : 0;
+                    if (STK) sek[STK ? sl : 0][STK ? 3 * ls + r : 0] = e;
+                    else if (r == NC - 1) sep[sl][ls] = e;
+                    else if (NC == 3) reinterpret_cast<float*>(&sel[sl][ls])[2 + r] = e;
+                    else reinterpret_cast<float*>(&sel2[NC == 5 ? sl : 0][NC == 5 ? ls : 0])[r] = e;
                 }
                 // the stick form's two thresholds, the interval's constants (every step's P and c0
                 // are the same): here, where the evaluations leave time, not in wave 2 -- its check
                 // sets the stick form's pace (profiles/r05/rprof_w2/)
-                if (STK && t == 0)
+                if (STK && t == 0 && sp == 0)
                     sthr[sl] = make_float2(phase_thr(pr, cb + (uint32_t)(1 - HC)), phase_thr(pr, cb + (uint32_t)(2 - HC)));
             } else {
                 if (!STK) {
                     for (int r = h; r < NC - 1; r += LPS)
-                        reinterpret_cast<float*>(&sel[sl][l])[r] = phase_thr(pr, cb + (uint32_t)(r + 1 - HC));
+                        reinterpret_cast<float*>(&sel[sl][ls])[r] = phase_thr(pr, cb + (uint32_t)(r + 1 - HC));
                 }
                 if (h == 0) {
-                    scb[sl][l] = cb - (uint32_t)HC;
-                    spr[sl][l] = pr;
+                    scb[sl][ls] = cb - (uint32_t)HC;
+                    spr[sl][ls] = pr;
                 }
             }
+          }
         };
         // E2: interval k's check.  Lane group g = t / NB replays batch g of the interval (BPI
         // batches) from the chain's state before it -- the chain's steps on the same candidate data,
@@ -773,72 +784,80 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 if (t == 0) smiss[sl] = k == inj ? 2 : any ? 1 : 0;
                 return;
             }
-            const int g = t / NB, lg = t & (NB - 1);
-            const bool act = g < BPI;
-            const int gb = act ? g : 0;  // the groups past the interval's batches replay batch 0
-            const float2 r0 = gb > 0 ? sst[sl][gb - 1] : sst[(k - 1) & 3][BPI - 1];
-            float ig = r0.x, ph = r0.y;
-            // step 0's candidate data: those of the trigArg before it (after an exactly redone
-            // interval that trigArg's exact e in every slot, as the chain's carry)
-            float4 ca, ca2;
-            float cep;
-            if (gb > 0) {
-                ca = cand(sl, NB * gb - 1);
-                cep = cand_ep(sl, NB * gb - 1);
-                ca2 = sel2[NC == 5 ? sl : 0][NC == 5 ? NB * gb - 1 : 0];
-            } else if (sexact[(k - 1) & 3]) {
-                const int j = j0(k);
-                const float e = exact_e((float)(pr_at(j - 1) + (double)ph), x[min(j, n - 1)]);
-                ca = NC == 3 ? make_float4(0.0f, 0.0f, e, e) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                ca2 = make_float4(e, e, e, e);
-                cep = e;
-            } else {
-                ca = cand((k - 1) & 3, NI - 1);
-                cep = cand_ep((k - 1) & 3, NI - 1);
-                ca2 = sel2[NC == 5 ? (k - 1) & 3 : 0][NC == 5 ? NI - 1 : 0];
-            }
-            // the batch's candidate data, read before the steps (the step loop then never waits on
-            // LDS); lane l keeps the phase of step l and checks its own trigArg afterwards
-            float4 da[NB], da2[NC == 5 ? NB : 1];
-            float dep[NB];
-            if constexpr (STK) {  // the batch's three e a step as 16-byte reads, the thresholds once
-                const float2 T = sthr[sl];
-                float ek[3 * NB];
-#pragma unroll
-                for (int q = 0; q < 3 * NB / 4; q++)
-                    *reinterpret_cast<float4*>(&ek[4 * q]) =
-                        reinterpret_cast<const float4*>(&sek[STK ? sl : 0][STK ? 3 * NB * gb : 0])[q];
-#pragma unroll
-                for (int j = 0; j < NB - 1; j++) {
-                    da[j] = make_float4(T.x, T.y, ek[3 * j], ek[3 * j + 1]);
-                    dep[j] = ek[3 * j + 2];
+            // 64 / NB lane groups a wave, so BPI > 64 / NB batches (128-step intervals) take rounds
+            constexpr int GPW = 64 / NB, RND = (BPI + GPW - 1) / GPW;
+            const int g0 = t / NB, lg = t & (NB - 1);
+            bool anybad = false;
+#pragma unroll 1
+            for (int rd = 0; rd < RND; rd++) {
+                const int g = g0 + GPW * rd;
+                const bool act = g < BPI;
+                const int gb = act ? g : 0;  // the groups past the interval's batches replay batch 0
+                const float2 r0 = gb > 0 ? sst[sl][gb - 1] : sst[(k - 1) & 3][BPI - 1];
+                float ig = r0.x, ph = r0.y;
+                // step 0's candidate data: those of the trigArg before it (after an exactly redone
+                // interval that trigArg's exact e in every slot, as the chain's carry)
+                float4 ca, ca2;
+                float cep;
+                if (gb > 0) {
+                    ca = cand(sl, NB * gb - 1);
+                    cep = cand_ep(sl, NB * gb - 1);
+                    ca2 = sel2[NC == 5 ? sl : 0][NC == 5 ? NB * gb - 1 : 0];
+                } else if (sexact[(k - 1) & 3]) {
+                    const int j = j0(k);
+                    const float e = exact_e((float)(pr_at(j - 1) + (double)ph), x[min(j, n - 1)]);
+                    ca = NC == 3 ? make_float4(0.0f, 0.0f, e, e) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    ca2 = make_float4(e, e, e, e);
+                    cep = e;
+                } else {
+                    ca = cand((k - 1) & 3, NI - 1);
+                    cep = cand_ep((k - 1) & 3, NI - 1);
+                    ca2 = sel2[NC == 5 ? (k - 1) & 3 : 0][NC == 5 ? NI - 1 : 0];
                 }
-            } else {
+                // the batch's candidate data, read before the steps (the step loop then never waits on
+                // LDS); lane l keeps the phase of step l and checks its own trigArg afterwards
+                float4 da[NB], da2[NC == 5 ? NB : 1];
+                float dep[NB];
+                if constexpr (STK) {  // the batch's three e a step as 16-byte reads, the thresholds once
+                    const float2 T = sthr[sl];
+                    float ek[3 * NB];
 #pragma unroll
-                for (int j = 0; j < NB - 1; j++) {
-                    da[j] = cand(sl, NB * gb + j);
-                    dep[j] = cand_ep(sl, NB * gb + j);
-                    if constexpr (NC == 5) da2[j] = sel2[NC == 5 ? sl : 0][NC == 5 ? NB * gb + j : 0];
+                    for (int q = 0; q < 3 * NB / 4; q++)
+                        *reinterpret_cast<float4*>(&ek[4 * q]) =
+                            reinterpret_cast<const float4*>(&sek[STK ? sl : 0][STK ? 3 * NB * gb : 0])[q];
+#pragma unroll
+                    for (int j = 0; j < NB - 1; j++) {
+                        da[j] = make_float4(T.x, T.y, ek[3 * j], ek[3 * j + 1]);
+                        dep[j] = ek[3 * j + 2];
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < NB - 1; j++) {
+                        da[j] = cand(sl, NB * gb + j);
+                        dep[j] = cand_ep(sl, NB * gb + j);
+                        if constexpr (NC == 5) da2[j] = sel2[NC == 5 ? sl : 0][NC == 5 ? NB * gb + j : 0];
+                    }
                 }
-            }
-            // pll_batch_fast's range test, on the state at the batch's start
-            const bool range_ok = fabsf(r0.y) < kPllMaxPhase && fabsf(r0.x) < kPllMaxInteg;
-            float mine = 0.0f;
+                // pll_batch_fast's range test, on the state at the batch's start
+                const bool range_ok = fabsf(r0.y) < kPllMaxPhase && fabsf(r0.x) < kPllMaxInteg;
+                float mine = 0.0f;
 #pragma unroll
-            for (int j = 0; j < NB; j++) {
-                const float e = NC == 3 ? pick(ph, j == 0 ? ca : da[j > 0 ? j - 1 : 0], j == 0 ? cep : dep[j > 0 ? j - 1 : 0])
-                                        : pick5(ph, j == 0 ? ca : da[j > 0 ? j - 1 : 0], j == 0 ? ca2 : da2[NC == 5 && j > 0 ? j - 1 : 0],
-                                                j == 0 ? cep : dep[j > 0 ? j - 1 : 0]);
-                const float2v kv = float2v{Ki, Kp} * e;
-                ig = ig + kv.x;
-                ph = ph + (kv.y + ig);
-                if (j == lg) mine = ph;
+                for (int j = 0; j < NB; j++) {
+                    const float e = NC == 3 ? pick(ph, j == 0 ? ca : da[j > 0 ? j - 1 : 0], j == 0 ? cep : dep[j > 0 ? j - 1 : 0])
+                                            : pick5(ph, j == 0 ? ca : da[j > 0 ? j - 1 : 0], j == 0 ? ca2 : da2[NC == 5 && j > 0 ? j - 1 : 0],
+                                                    j == 0 ? cep : dep[j > 0 ? j - 1 : 0]);
+                    const float2v kv = float2v{Ki, Kp} * e;
+                    ig = ig + kv.x;
+                    ph = ph + (kv.y + ig);
+                    if (j == lg) mine = ph;
+                }
+                const int J = NB * gb + lg;  // this lane's step
+                const float a = (float)(spr[sl][J] + (double)mine);
+                const bool bad = verdict(sl, J, a) || !range_ok;
+                if (act) out[j0(k) + J] = a;
+                anybad = anybad || (act && bad);
             }
-            const int J = NB * gb + lg;  // this lane's step
-            const float a = (float)(spr[sl][J] + (double)mine);
-            const bool bad = verdict(sl, J, a) || !range_ok;
-            if (act) out[j0(k) + J] = a;
-            const bool any = __builtin_amdgcn_ballot_w64(act && bad) != 0 || k == min(miss, ni);
+            const bool any = __builtin_amdgcn_ballot_w64(anybad) != 0 || k == min(miss, ni);
             // test hooks: a forced miss (the redo path); inject's is counted as resumed
             if (t == 0) smiss[sl] = k == inj ? 2 : any ? 1 : 0;
         };
@@ -874,14 +893,14 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                             __syncthreads();  // B1: the chain's exact redo of i - 2 follows
                             __syncthreads();  // B1.5: i - 2's exact end state is in the ring
                             {
-                                float v;
+                                float v[SPL];
                                 ld(i, v);
                                 put(i, sst[(i - 2) & 3][BPI - 1].y, v);
                             }
                             __syncthreads();  // B2: the chain ran i - 1 again
                             check(i - 1);
                             if (i + 1 <= ni) {  // interval i + 1 from the phase at i's start
-                                float v;
+                                float v[SPL];
                                 ld(i + 1, v);
                                 put(i + 1, sst[(i - 1) & 3][BPI - 1].y, v);
                             }
@@ -1785,6 +1804,12 @@ void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_str
                        seg, step, norm_bw, st, out, ostride, fail, rec, rb, inject, sat_ok, pipe_on);
 }
 
+#ifndef FMRX_STICK_BPI
+#define FMRX_STICK_BPI 8  // batches an interval of the stick form: 128-step intervals (4: 64)
+#endif
+#ifndef FMRX_PIPE22_BPI
+#define FMRX_PIPE22_BPI 8  // batches an interval of the three-candidate form below the stick (128 steps)
+#endif
 #ifndef FMRX_PIPE_RD
 #define FMRX_PIPE_RD 8  // intervals of step inputs in flight (the evaluators' loop is unrolled by it)
 #endif
@@ -1796,10 +1821,10 @@ void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_
 #endif
     if (n <= 0) return;
     if (form == 23)
-        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, FMRX_PIPE_RD, 3, true>), dim3(n_streams), dim3(192), 0, s, io, n,
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, FMRX_STICK_BPI, FMRX_PIPE_RD, 3, true>), dim3(n_streams), dim3(192), 0, s, io, n,
                            n_streams, stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
     else if (form == 22)
-        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, FMRX_PIPE_RD, 3>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, FMRX_PIPE22_BPI, FMRX_PIPE_RD, 3>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
                            stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
     else if (form == 21)
         hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, FMRX_PIPE_RD, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
