@@ -578,7 +578,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                                                       size_t ostride, int inject, int miss,
                                                       unsigned long long* stats, unsigned* redos) {
     constexpr int NI = NB * BPI;
-    static_assert(NI == 16 || NI == 32 || NI == 64 || (NC == 3 && NI == 128),
+    static_assert(NI == 16 || NI == 32 || NI == 64 || (BPI > 1 && NI == 128),
                   "the evaluators' lane map: 64 / NI lanes a step, or NI / 64 steps a lane");
     static_assert(NC == 3 || NC == 5, "three or five candidates");
     // STK: the stuck trigOffset (2^24, filter.cpp:165-166: 69.9 s into a stream).  Every step's
@@ -646,7 +646,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     // intervals in [2^21, 2^22), with 16-step ones in [2^20, 2^21)
     const bool in_domain = STK ? pll_pipe_stream(p.trig, step, kPllTrigStick)
                          : NC == 3 ? pll_pipe_stream(p.trig, step, kPllPipeMin)
-                                   : NI == 64 ? pll_pipe_stream(p.trig, step, kPllPipeMin5, kPllPipeMin - 1.0f)
+                                   : NI >= 64 ? pll_pipe_stream(p.trig, step, kPllPipeMin5, kPllPipeMin - 1.0f)
                                               : pll_pipe_stream(p.trig, step, kPllPipeMinLow, kPllPipeMin5 - 1.0f);
     const float trig0 = p.trig;
     const double t0d = (double)trig0;
@@ -1477,7 +1477,8 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
     constexpr int NT = (NI * (NC + 1) + EV - 1) / EV;  // threshold items a lane an interval
     constexpr int CH = NI < 16 ? NI : 16;          // the chain's steps a burst of reads
     static_assert(NC % 2 == 1 && NP <= 64, "an odd window within a wave");
-    static_assert(NI == 16 || NI == 32 || NI == 64, "a row of counts in a VGPR");
+    static_assert(NI == 16 || NI == 32 || NI == 64 || NI == 128, "the counts in one or two VGPR rows");
+    constexpr int NRW = NI > 64 ? 2 : 1;  // rows of counts: step J in lane J & 63 of row J >> 6
     // rings of four intervals (interval k in slot k & 3): the T and E rows of each pair of steps
     // interleaved by row slot (sR[.][p][l] = T_2p(l), E_2p(l), T_2p+1(l), E_2p+1(l): one 16-byte
     // read a lane gives the chain two steps' rows), bits(c_base) - 1 of each step (the trigArg
@@ -1584,7 +1585,11 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
             if (w != 1) return;
             const int sl = k & 3;
             if (sexact[sl]) return;
-            if (t < NI) out[j0(k) + t] = __builtin_bit_cast(float, sbase[sl][t] + (uint32_t)srow[sl][t]);
+#pragma unroll
+            for (int r = 0; r < NRW; r++) {
+                const int J = t + 64 * r;
+                if (J < NI) out[j0(k) + J] = __builtin_bit_cast(float, sbase[sl][J] + (uint32_t)srow[sl][J]);
+            }
         };
 #pragma unroll
         for (int u = 0; u < RD; u++) ld(1 + u, vq[(1 + u) % RD]);
@@ -1650,7 +1655,7 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
         const unsigned long long p0 = PROF_T();
         const int is = i & 3;
         const float integ0 = integ, phase0 = phase;
-        int row = 0;
+        int row[NRW] = {};
         unroll_ic(
             [&](auto hc) {
                 constexpr int H = decltype(hc)::value;
@@ -1676,10 +1681,10 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
                         // the count of thresholds the phase reaches: trigArg's place in the window + 1
                         cC = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(phase >= T[J]));
                         cE = E[J];
-                        int rw = row;
+                        int rw = row[(H * CH + J) >> 6];
                         const uint32_t sc = cC;
-                        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(rw) : "s"(sc), "i"(H * CH + J));
-                        row = rw;
+                        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(rw) : "s"(sc), "i"((H * CH + J) & 63));
+                        row[(H * CH + J) >> 6] = rw;
                     },
                     std::make_integer_sequence<int, CH>{});
             },
@@ -1702,7 +1707,9 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
             phase = q.phase;
             carry_exact((float)c.x, i + 1);
         }
-        if (t < NI) srow[is][t] = row;
+#pragma unroll
+        for (int r = 0; r < NRW; r++)
+            if (t + 64 * r < NI) srow[is][t + 64 * r] = row[r];
         sst[is] = make_float2(integ, phase);
         sexact[is] = bad ? 1 : 0;
         const unsigned long long p1 = PROF_T();
@@ -1810,6 +1817,9 @@ void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_str
 #ifndef FMRX_PIPE22_BPI
 #define FMRX_PIPE22_BPI 8  // batches an interval of the three-candidate form below the stick (128 steps)
 #endif
+#ifndef FMRX_PIPE21_BPI
+#define FMRX_PIPE21_BPI 8  // batches an interval of the five-candidate [2^21, 2^22) form (128 steps)
+#endif
 #ifndef FMRX_PIPE_RD
 #define FMRX_PIPE_RD 8  // intervals of step inputs in flight (the evaluators' loop is unrolled by it)
 #endif
@@ -1827,7 +1837,7 @@ void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_
         hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, FMRX_PIPE22_BPI, FMRX_PIPE_RD, 3>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
                            stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
     else if (form == 21)
-        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 4, FMRX_PIPE_RD, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, FMRX_PIPE21_BPI, FMRX_PIPE_RD, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
                            stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
     else
         hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 1, FMRX_PIPE_RD, 5>), dim3(n_streams), dim3(192), 0, s, io, n, n_streams,
@@ -1899,6 +1909,9 @@ static int cnt_launch(hipStream_t s, const float* io, int n, int n_streams, size
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+#ifndef FMRX_CNT20_NI
+#define FMRX_CNT20_NI 64  // steps an interval of the [2^20, 2^21) count form
+#endif
 #ifndef FMRX_CNT_NW
 #define FMRX_CNT_NW 4  // evaluator waves of the [2^19, 2^21) count forms
 #endif
@@ -1920,7 +1933,7 @@ int launch_pll_cnt(hipStream_t s, const float* io, int n, int n_streams, size_t 
             return cnt_launch<32, 15, FMRX_CNT_NW>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
                                          524288.0f, 1048575.0f, stats, redos);
         case 20:
-            return cnt_launch<64, 15, FMRX_CNT_NW>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
+            return cnt_launch<FMRX_CNT20_NI, 15, FMRX_CNT_NW>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
                                          kPllPipeMinLow, kPllPipeMin5 - 1.0f, stats, redos);
         default:  // three waves a stream, as the three-wave runner it would replace
             return cnt_launch<64, 7, 2>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
