@@ -1910,7 +1910,7 @@ static int cnt_launch(hipStream_t s, const float* io, int n, int n_streams, size
 }
 
 #ifndef FMRX_CNT20_NI
-#define FMRX_CNT20_NI 64  // steps an interval of the [2^20, 2^21) count form
+#define FMRX_CNT20_NI 128  // steps an interval of the [2^20, 2^21) count form (two rows of counts)
 #endif
 #ifndef FMRX_CNT_NW
 #define FMRX_CNT_NW 4  // evaluator waves of the [2^19, 2^21) count forms
