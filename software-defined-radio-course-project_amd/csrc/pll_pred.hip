@@ -1909,6 +1909,9 @@ static int cnt_launch(hipStream_t s, const float* io, int n, int n_streams, size
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+#ifndef FMRX_CNT19_NI
+#define FMRX_CNT19_NI 32  // steps an interval of the [2^19, 2^20) count form
+#endif
 #ifndef FMRX_CNT20_NI
 #define FMRX_CNT20_NI 128  // steps an interval of the [2^20, 2^21) count form (two rows of counts)
 #endif
@@ -1930,7 +1933,7 @@ int launch_pll_cnt(hipStream_t s, const float* io, int n, int n_streams, size_t 
             return cnt_launch<16, 31, 4>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
                                          262144.0f, 524287.0f, stats, redos);
         case 19:
-            return cnt_launch<32, 15, FMRX_CNT_NW>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
+            return cnt_launch<FMRX_CNT19_NI, 15, FMRX_CNT_NW>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
                                          524288.0f, 1048575.0f, stats, redos);
         case 20:
             return cnt_launch<FMRX_CNT20_NI, 15, FMRX_CNT_NW>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
