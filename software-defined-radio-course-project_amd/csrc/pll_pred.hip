@@ -1910,7 +1910,7 @@ static int cnt_launch(hipStream_t s, const float* io, int n, int n_streams, size
 }
 
 #ifndef FMRX_CNT19_NI
-#define FMRX_CNT19_NI 32  // steps an interval of the [2^19, 2^20) count form
+#define FMRX_CNT19_NI 64  // steps an interval of the [2^19, 2^20) count form
 #endif
 #ifndef FMRX_CNT20_NI
 #define FMRX_CNT20_NI 128  // steps an interval of the [2^20, 2^21) count form (two rows of counts)

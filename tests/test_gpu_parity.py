@@ -847,15 +847,16 @@ def test_pll_predicted_runner(fmrx, orc, monkeypatch, trig0, inject, pred, pipe)
 
 
 @pytest.mark.parametrize("trig0", [1048600.0, 2097185.0, 4194321.0, 16772216.0, 16777216.0])
-@pytest.mark.parametrize("miss", ["1", "2", "150", "311", "312", "1248", "5000"])
+@pytest.mark.parametrize("miss", ["1", "2", "77", "155", "156", "311", "312", "1248", "5000"])
 @pytest.mark.parametrize("stick", [1, 0])
 def test_pll_pipe_redo(fmrx, orc, monkeypatch, trig0, miss, stick):
     """The three-wave runner's miss path (pll_pipe_kernel): knob pll_pipe_miss=k makes its check
     report interval k as missed (past the last interval: the last), so the chain redoes that
     interval and the two after it exactly and the evaluators restart from the corrected phase.
-    20,000 steps = batch 0 + 312 intervals of 64 steps + 1 batch from 2^21 (k = 1, 150, 311 and
-    312: the first, a middle one and the verdicts read after the loop), batch 0 + 1,249 intervals
-    of 16 steps in [2^20, 2^21) (1,248 and 1,249 the last two).  From the stuck trigOffset 2^24
+    20,000 steps = batch 0 + 156 intervals of 128 steps + 1 batch from 2^21 (k = 1, 77, 155 and
+    156: the first, a middle one and the verdicts read after the loop; larger k: the last), and in
+    [2^20, 2^21) the count runner's 128-step intervals or, with pll_cnt = 0, the 16-step form's
+    1,249 (1,248 and 1,249 the last two).  From the stuck trigOffset 2^24
     (and 5,000 steps before it: the handover inside the call) the stick form (knob pll_stick = 1:
     the interval's two thresholds once, three e a step) or the plain three-candidate form (0).
     Bit-exact, every batch verifies."""
