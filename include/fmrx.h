@@ -263,7 +263,9 @@ int fmrx_debug_stage_timing(fmrx_ctx* ctx, int op, double* ms, double* steps, lo
 #define FMRX_KNOB_PLL_STICK 13        /* 1: the stick form past trigOffset 2^24         FMRX_PLL_STICK */
 #define FMRX_KNOB_STEREO_HEAD 14      /* first chunk in 16ths of a chunk (8)          FMRX_STEREO_HEAD */
 #define FMRX_KNOB_STEREO_LEAD 15      /* n: chunk k's front end after chunk k-n's PLL  FMRX_STEREO_LEAD */
-#define FMRX_KNOB_AUDIO_DEFER 16      /* 1: every chunk's audio after the last PLL (1) FMRX_AUDIO_DEFER */
+#define FMRX_KNOB_AUDIO_DEFER 16      /* 0 beside the next PLL, 1 after the last, 2 (default) all but the
+                                         last chunk's beside the last PLL           FMRX_AUDIO_DEFER */
+#define FMRX_KNOB_STEREO_TAIL 17      /* last chunk in 16ths of a chunk (8)          FMRX_STEREO_TAIL */
 int fmrx_debug_set_knob(fmrx_ctx* ctx, int knob, double value);
 
 #ifdef __cplusplus

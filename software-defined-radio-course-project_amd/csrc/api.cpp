@@ -135,8 +135,9 @@ struct fmrx_ctx {
         PllKnobs pll;
         int stereo_chunks = 0;  // 0: by stream count and call length; k: k chunks (1: serial engine)
         int stereo_head = 8;    // the first chunk's blocks in 16ths of a middle chunk's
+        int stereo_tail = 8;    // the last chunk's blocks in 16ths of a middle chunk's
         int stereo_lead = 0;    // n > 0: chunk k's front end waits for chunk k - n's PLL; 0: none
-        int audio_defer = 1;    // every chunk's audio stage after the last chunk's PLL (its NCO not); 0: beside
+        int audio_defer = 2;    // 2: chunks 0 .. K-2's audio beside the last PLL; 1: all after it; 0: beside the next
         int mono_split = -1;    // -1: kOlderShare; 0: equal spans; n: the older wave's n / 1024
         int bpf_tile = 1;       // 0: the per-output band-pass kernel
         int halo_kernel = 0;    // 1: the separate halo_kernel after the fused one
@@ -479,15 +480,16 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
     return 0;
 }
 
-// First block of chunk k of K (k = K: n_blocks).  The last chunk is half the others and the first
-// head / 16 of one (knob stereo_head, default 8: half): the first chunk's front end and the last
-// chunk's NCO and audio stage have no PLL beside them.
-size_t chunk_begin(size_t n_blocks, int k, int K, int head = 8) {
+// First block of chunk k of K (k = K: n_blocks).  The first chunk is head / 16 of the others and
+// the last tail / 16 (knobs stereo_head, stereo_tail; default 8: half): the first chunk's front
+// end and the last chunk's NCO and audio stage have no PLL beside them.
+size_t chunk_begin(size_t n_blocks, int k, int K, int head = 8, int tail = 8) {
     if (K <= 1 || k <= 0) return k <= 0 ? 0 : n_blocks;
     if (k >= K) return n_blocks;
     const unsigned long long h = (unsigned long long)std::max(1, std::min(head, 64));
+    const unsigned long long tl = (unsigned long long)std::max(1, std::min(tail, 64));
     return (size_t)(((unsigned long long)n_blocks * (h + 16ULL * (unsigned long long)(k - 1))) /
-                    (h + 16ULL * (unsigned long long)(K - 2) + 8ULL));
+                    (h + 16ULL * (unsigned long long)(K - 2) + tl));
 }
 
 // Chunks of the stereo pipeline for a call of n_blocks blocks a stream: the stage work beside
@@ -504,7 +506,8 @@ int stereo_chunks(const fmrx_ctx* c, size_t n_blocks) {
     const size_t hb = (c->halo_bytes + c->geo.block_bytes - 1) / c->geo.block_bytes;
     auto short_chunk = [&](int kk) {  // a chunk of the partition shorter than the halo
         for (int j = 0; j < kk; j++)
-            if (chunk_begin(n_blocks, j + 1, kk, c->knobs.stereo_head) - chunk_begin(n_blocks, j, kk, c->knobs.stereo_head) < hb)
+            if (chunk_begin(n_blocks, j + 1, kk, c->knobs.stereo_head, c->knobs.stereo_tail) -
+                    chunk_begin(n_blocks, j, kk, c->knobs.stereo_head, c->knobs.stereo_tail) < hb)
                 return true;
         return false;
     };
@@ -546,10 +549,12 @@ int run_stereo_pipelined(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int1
 
 int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks, int16_t* d_pcm, float* d_mono,
                               int K) {
+    // first block of chunk j of K
+    auto cb = [&](int j) { return chunk_begin(n_blocks, j, K, c->knobs.stereo_head, c->knobs.stereo_tail); };
     const int ns = c->cfg.n_streams;
     const size_t ipb = c->geo.if_samples, n_if = n_blocks * ipb;
     for (int k = 0; k < K; k++)
-        if ((chunk_begin(n_blocks, k + 1, K, c->knobs.stereo_head) - chunk_begin(n_blocks, k, K, c->knobs.stereo_head)) * c->geo.block_bytes < c->halo_bytes)
+        if ((cb(k + 1) - cb(k)) * c->geo.block_bytes < c->halo_bytes)
             return fail(FMRX_EINVAL, "chunks shorter than the halo");
     int rc = c->d_channel.ensure(n_if * ns);
     if (!rc) rc = c->d_carrier.ensure(n_if * ns);
@@ -576,7 +581,7 @@ int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks,
     HIPCHK(hipStreamWaitEvent(c->s_audio, ev_start, 0));
     size_t max_m = 0;
     for (int k = 0; k < K; k++)
-        max_m = std::max(max_m, (chunk_begin(n_blocks, k + 1, K, c->knobs.stereo_head) - chunk_begin(n_blocks, k, K, c->knobs.stereo_head)) * ipb);
+        max_m = std::max(max_m, (cb(k + 1) - cb(k)) * ipb);
     if ((rc = c->d_pll_side.ensure(pll_side_doubles((int)max_m, ns)))) return rc;
     if ((rc = c->d_pll_side2.ensure(pll_side_doubles((int)max_m, ns)))) return rc;
     AudioLaunch A{};
@@ -617,8 +622,16 @@ int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks,
         c->pll_trig.advance(m);
         return 0;
     };
+    // the audio stage of chunk j (s_audio, after chunk j's NCO)
+    auto audio = [&](int j) -> int {
+        const int t_au = c->stage_timer.begin(c->s_audio);
+        if (launch_stereo_audio_range(A, (int)cb(j), (int)cb(j + 1), j == K - 1, ns, c->s_audio))
+            return fail(FMRX_EHIP, "stereo audio launch failed");
+        c->stage_timer.end(t_au, kStAudio, 0.0, c->s_audio);
+        return 0;
+    };
     for (int k = 0; k < K; k++) {
-        const size_t b0 = chunk_begin(n_blocks, k, K, c->knobs.stereo_head), b1 = chunk_begin(n_blocks, k + 1, K, c->knobs.stereo_head);
+        const size_t b0 = cb(k), b1 = cb(k + 1);
         const size_t nb = b1 - b0, m = nb * ipb, off = b0 * ipb;
         const bool last = k == K - 1;
         if (k == 1 && lane_m > 0) HIPCHK(hipStreamWaitEvent(c->s_front, ev_lane, 0));
@@ -660,26 +673,22 @@ int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks,
             return fail(FMRX_EHIP, "NCO launch failed");
         c->stage_timer.end(t_nco, kStNco, 0.0, c->s_audio);
         HIPCHK(hipEventRecord(ev_nco(k), c->s_audio));
-        // (audio_defer, the default: the audio stages after the loop -- their LDS tiles then never
-        // run beside a PLL chain, whose LDS reads they slow (tools/ubench_noise.hip); configs[4]
-        // 0.4168 -> 0.4113 s, profiles/r05/ab_audio_defer/)
-        if (!c->knobs.audio_defer) {
-            const int t_au = c->stage_timer.begin(c->s_audio);
-            if (launch_stereo_audio_range(A, (int)b0, (int)b1, last, ns, c->s_audio))
-                return fail(FMRX_EHIP, "stereo audio launch failed");
-            c->stage_timer.end(t_au, kStAudio, 0.0, c->s_audio);
-        }
+        // audio_defer (tools/ubench_noise.hip: the audio stages' LDS tiles slow the PLL chains they
+        // run beside): 0 each chunk's audio after its NCO, beside the next chunk's PLL; 1 every
+        // chunk's after the last chunk's PLL (configs[4] 0.4168 -> 0.4113 s,
+        // profiles/r05/ab_audio_defer/); 2, the default, chunks 0 .. K - 2 beside the LAST chunk's
+        // PLL only and chunk K - 1's after it: a short tail, one chunk's chains disturbed
+        // (0.4058 -> 0.3955 s, profiles/r05/ab_audio_defer2/)
+        const int ad = c->knobs.audio_defer;
+        if (ad == 0 && (rc = audio(k))) return rc;
+        if (ad == 2 && k == K - 2)
+            for (int j = 0; j <= K - 2; j++)
+                if ((rc = audio(j))) return rc;
+        if (ad == 2 && k == K - 1 && (rc = audio(k))) return rc;
     }
-    if (c->knobs.audio_defer) {
-        for (int k = 0; k < K; k++) {
-            const int t_au = c->stage_timer.begin(c->s_audio);
-            if (launch_stereo_audio_range(A, (int)chunk_begin(n_blocks, k, K, c->knobs.stereo_head),
-                                          (int)chunk_begin(n_blocks, k + 1, K, c->knobs.stereo_head), k == K - 1, ns,
-                                          c->s_audio))
-                return fail(FMRX_EHIP, "stereo audio launch failed");
-            c->stage_timer.end(t_au, kStAudio, 0.0, c->s_audio);
-        }
-    }
+    if (c->knobs.audio_defer == 1)
+        for (int j = 0; j < K; j++)
+            if ((rc = audio(j))) return rc;
     // demod history for the next call (after every read of this call's demod: the last audio
     // launch follows every band-pass launch through the events)
     if (launch_copy_streams(c->d_demod.p, c->demod_stride, c->d_demod.p + n_if, c->demod_stride, kDemodHist, ns,
@@ -784,8 +793,9 @@ static fmrx_ctx::Knobs knobs_from_env() {
     k.pll.stick = get("FMRX_PLL_STICK", 1);
     k.stereo_chunks = std::max(0, get("FMRX_STEREO_CHUNKS", 0));
     k.stereo_head = std::max(1, get("FMRX_STEREO_HEAD", 8));
+    k.stereo_tail = std::max(1, get("FMRX_STEREO_TAIL", 8));
     k.stereo_lead = std::max(0, get("FMRX_STEREO_LEAD", 0));
-    k.audio_defer = get("FMRX_AUDIO_DEFER", 1);
+    k.audio_defer = get("FMRX_AUDIO_DEFER", 2);
     k.mono_split = get("FMRX_MONO_SPLIT", -1);
     k.bpf_tile = get("FMRX_BPF_TILE", 1);
     k.halo_kernel = get("FMRX_HALO_KERNEL", 0);
@@ -1491,6 +1501,7 @@ int fmrx_debug_set_knob(fmrx_ctx* c, int knob, double value) {
         case FMRX_KNOB_PLL_IDX: k.pll.idx = v; break;
         case FMRX_KNOB_STEREO_CHUNKS: k.stereo_chunks = std::max(0, v); break;
         case FMRX_KNOB_STEREO_HEAD: k.stereo_head = std::max(1, v); break;
+        case FMRX_KNOB_STEREO_TAIL: k.stereo_tail = std::max(1, v); break;
         case FMRX_KNOB_STEREO_LEAD: k.stereo_lead = std::max(0, v); break;
         case FMRX_KNOB_AUDIO_DEFER: k.audio_defer = v; break;
         case FMRX_KNOB_MONO_SPLIT: k.mono_split = v; break;

@@ -489,7 +489,8 @@ def test_stereo_multistream(fmrx, orc):
 @pytest.mark.parametrize("mode,n_streams,nb,chunks,lead", [(0, 5, 48, "3", 0), (0, 1, 64, "4", 0), (1, 3, 40, "2", 0),
                                                            (2, 2, 3, "2", 0), (0, 70, 120, None, 0),
                                                            (0, 5, 48, "4", 1), (0, 70, 120, None, 2),
-                                                           (0, 70, 120, None, -1), (1, 3, 40, "2", -1)])
+                                                           (0, 70, 120, None, -1), (1, 3, 40, "2", -1),
+                                                           (0, 70, 120, None, -2), (0, 5, 48, "4", -2)])
 def test_stereo_pipelined_chunks(fmrx, orc, monkeypatch, mode, n_streams, nb, chunks, lead):
     """The pipelined stereo engine (api.cpp run_stereo_pipelined): a call's blocks in chunks,
     front end + band-pass of chunk k + 1 and audio of chunk k - 1 on their own HIP streams beside
@@ -497,9 +498,10 @@ def test_stereo_pipelined_chunks(fmrx, orc, monkeypatch, mode, n_streams, nb, ch
     is the call's own bytes in front of it).  knob stereo_chunks forces the chunk count (None: the
     default, 8 from 16 streams, fewer when a chunk would hold < 2^14 samples); two calls in a row
     check the carried state.  Modes 0/1 take the tiled audio kernel, mode 2 the per-frame one.
-    lead > 0: the paced schedule (chunk k's front end after chunk k - lead's PLL); -1: every
-    chunk's audio stage deferred past the last PLL (knob audio_defer)."""
-    kw = {"stereo_lead": float(max(lead, 0)), "audio_defer": float(lead < 0)}
+    lead > 0: the paced schedule (chunk k's front end after chunk k - lead's PLL); lead <= 0: knob
+    audio_defer = -lead (0 each chunk's audio beside the next PLL, 1 every chunk's after the last
+    PLL, 2 all but the last chunk's beside the last PLL)."""
+    kw = {"stereo_lead": float(max(lead, 0)), "audio_defer": float(max(-lead, 0))}
     if chunks is not None:
         kw["stereo_chunks"] = float(chunks)
     knobs(monkeypatch, fmrx, **kw)
