@@ -517,6 +517,20 @@ def test_stereo_pipelined_chunks(fmrx, orc, monkeypatch, mode, n_streams, nb, ch
         assert np.array_equal(np.concatenate([a[s], b[s]]), want), s
 
 
+@pytest.mark.parametrize("head,tail", [(8, 2), (2, 16), (16, 1)])
+def test_stereo_pipelined_head_tail(fmrx, orc, monkeypatch, head, tail):
+    """The pipelined engine's first and last chunk sizes (knobs stereo_head / stereo_tail, in 16ths
+    of a middle chunk): 70 streams, the default 8 chunks, bit-exact against the oracle."""
+    knobs(monkeypatch, fmrx, stereo_head=float(head), stereo_tail=float(tail))
+    n_streams, nb, bb = 70, 120, 12800
+    recipes = [("synth:%d" if s % 3 else "rand:%d") % (600 + s) for s in range(n_streams)]
+    ins = np.stack([iqgen.make(r, nb * bb) for r in recipes])
+    with fmrx.Receiver(0, fmrx.STEREO, n_streams=n_streams) as rx:
+        out = np.atleast_2d(rx.process(ins))
+    for s in (0, 35, 69):
+        assert np.array_equal(out[s], orc.run(0, 51, ins[s], ["pcm"])["pcm"]), s
+
+
 def test_stereo_pipelined_checkpoint_resume(fmrx, orc, monkeypatch):
     """The pipelined engine's carried state (demod history, PLL with its trigOffset hint, mixer
     tail, mono delay; api.cpp run_stereo_pipelined) through a checkpoint: 16 streams (the
