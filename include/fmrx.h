@@ -266,7 +266,6 @@ int fmrx_debug_stage_timing(fmrx_ctx* ctx, int op, double* ms, double* steps, lo
 #define FMRX_KNOB_AUDIO_DEFER 16      /* 0 beside the next PLL, 1 after the last, 2 (default) all but the
                                          last chunk's beside the last PLL           FMRX_AUDIO_DEFER */
 #define FMRX_KNOB_STEREO_TAIL 17      /* last chunk in 16ths of a chunk (8)          FMRX_STEREO_TAIL */
-#define FMRX_KNOB_STEREO_GATE 18      /* g: front ends of chunks >= g after PLL g-2  FMRX_STEREO_GATE */
 int fmrx_debug_set_knob(fmrx_ctx* ctx, int knob, double value);
 
 #ifdef __cplusplus

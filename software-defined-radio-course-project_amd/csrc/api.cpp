@@ -136,7 +136,6 @@ struct fmrx_ctx {
         int stereo_chunks = 0;  // 0: by stream count and call length; k: k chunks (1: serial engine)
         int stereo_head = 8;    // the first chunk's blocks in 16ths of a middle chunk's
         int stereo_tail = 8;    // the last chunk's blocks in 16ths of a middle chunk's
-        int stereo_gate = 0;    // g >= 2: the front ends of chunks g .. K - 1 after chunk g - 2's PLL
         int stereo_lead = 0;    // n > 0: chunk k's front end waits for chunk k - n's PLL; 0: none
         int audio_defer = 2;    // 2: chunks 0 .. K-2's audio beside the last PLL; 1: all after it; 0: beside the next
         int mono_split = -1;    // -1: kOlderShare; 0: equal spans; n: the older wave's n / 1024
@@ -639,9 +638,6 @@ int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks,
         // paced: chunk k's front end runs beside chunk k - lead + 1's PLL, not all of them at the start
         const int lead = c->knobs.stereo_lead;
         if (lead > 0 && k >= lead) HIPCHK(hipStreamWaitEvent(c->s_front, ev_pll(k - lead), 0));
-        // gated: the front ends of chunks g and later wait, all together, for chunk g - 2's PLL
-        const int gate = c->knobs.stereo_gate;
-        if (gate >= 2 && k == gate) HIPCHK(hipStreamWaitEvent(c->s_front, ev_pll(gate - 2), 0));
         // s_front: front end and band-pass pair of chunk k
         if ((rc = run_fused(c, d_iq, nb, nullptr, nullptr, c->d_demod.p, c->demod_stride, kDemodHist, false, b0,
                             n_blocks, c->s_front, last)))
@@ -798,7 +794,6 @@ static fmrx_ctx::Knobs knobs_from_env() {
     k.stereo_chunks = std::max(0, get("FMRX_STEREO_CHUNKS", 0));
     k.stereo_head = std::max(1, get("FMRX_STEREO_HEAD", 8));
     k.stereo_tail = std::max(1, get("FMRX_STEREO_TAIL", 8));
-    k.stereo_gate = std::max(0, get("FMRX_STEREO_GATE", 0));
     k.stereo_lead = std::max(0, get("FMRX_STEREO_LEAD", 0));
     k.audio_defer = get("FMRX_AUDIO_DEFER", 2);
     k.mono_split = get("FMRX_MONO_SPLIT", -1);
@@ -1507,7 +1502,6 @@ int fmrx_debug_set_knob(fmrx_ctx* c, int knob, double value) {
         case FMRX_KNOB_STEREO_CHUNKS: k.stereo_chunks = std::max(0, v); break;
         case FMRX_KNOB_STEREO_HEAD: k.stereo_head = std::max(1, v); break;
         case FMRX_KNOB_STEREO_TAIL: k.stereo_tail = std::max(1, v); break;
-        case FMRX_KNOB_STEREO_GATE: k.stereo_gate = std::max(0, v); break;
         case FMRX_KNOB_STEREO_LEAD: k.stereo_lead = std::max(0, v); break;
         case FMRX_KNOB_AUDIO_DEFER: k.audio_defer = v; break;
         case FMRX_KNOB_MONO_SPLIT: k.mono_split = v; break;

@@ -103,7 +103,7 @@ STAGES = ["front_end", "bandpass_pair", "pll_prep", "runner_lane", "runner_pred"
 KNOBS = {"pll_spec": 0, "pll_sat": 1, "pll_pred": 2, "pll_pipe": 3, "pll_idx": 4, "stereo_chunks": 5,
          "mono_split": 6, "bpf_tile": 7, "halo_kernel": 8, "pll_inject": 9, "pll_pipe_miss": 10,
          "pll_hint_skew": 11, "pll_cnt": 12, "pll_stick": 13, "stereo_head": 14,
-         "stereo_lead": 15, "audio_defer": 16, "stereo_tail": 17, "stereo_gate": 18}
+         "stereo_lead": 15, "audio_defer": 16, "stereo_tail": 17}
 # knobs every new Receiver applies after fmrx_create (tests set it per test, e.g. with
 # monkeypatch.setattr; the library itself reads only the tuning knobs' environment variables)
 DEFAULT_KNOBS: dict = {}

@@ -154,6 +154,6 @@ def test_product_library_reads_no_output_changing_hook(fmrx):
     assert not names & hooks, names & hooks
     tuning = {b"FMRX_PLL_SPEC", b"FMRX_PLL_SAT", b"FMRX_PLL_PRED", b"FMRX_PLL_PIPE", b"FMRX_PLL_IDX",
               b"FMRX_STEREO_CHUNKS", b"FMRX_MONO_SPLIT", b"FMRX_BPF_TILE", b"FMRX_HALO_KERNEL", b"FMRX_MONO_VARIANT",
-              b"FMRX_PLL_CNT", b"FMRX_PLL_STICK", b"FMRX_STEREO_HEAD", b"FMRX_STEREO_LEAD", b"FMRX_AUDIO_DEFER", b"FMRX_STEREO_TAIL", b"FMRX_STEREO_GATE"}
+              b"FMRX_PLL_CNT", b"FMRX_PLL_STICK", b"FMRX_STEREO_HEAD", b"FMRX_STEREO_LEAD", b"FMRX_AUDIO_DEFER", b"FMRX_STEREO_TAIL"}
     assert names <= tuning, names - tuning
     assert set(fmrx.KNOBS) >= {"pll_inject", "pll_pipe_miss", "pll_hint_skew"}
