@@ -578,7 +578,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                                                       size_t ostride, int inject, int miss,
                                                       unsigned long long* stats, unsigned* redos) {
     constexpr int NI = NB * BPI;
-    static_assert(NI == 16 || NI == 32 || NI == 64 || (BPI > 1 && (NI == 128 || NI == 256)),
+    static_assert(NI == 16 || NI == 32 || NI == 64 || (BPI > 1 && (NI == 128 || NI == 256 || (STK && NI == 512))),
                   "the evaluators' lane map: 64 / NI lanes a step, or NI / 64 steps a lane");
     static_assert(NC == 3 || NC == 5, "three or five candidates");
     // STK: the stuck trigOffset (2^24, filter.cpp:165-166: 69.9 s into a stream).  Every step's
@@ -602,9 +602,9 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     // of c0 + 2 (sep); bits(c0) - HC (scb), P (spr); the certification of each candidate's e
     // (scert, byte r for c0 - HC + r); the chain's (integ, phase) at the end of each batch (sst);
     // per interval the check's verdict (smiss) and "redone exactly" (sexact)
-    __shared__ float4 sel[4][NI];
+    __shared__ float4 sel[STK ? 1 : 4][STK ? 1 : NI];  // (the stick form: sthr and sek instead)
     __shared__ float4 sel2[NC == 5 ? 4 : 1][NC == 5 ? NI : 1];
-    __shared__ float sep[4][NI];
+    __shared__ float sep[STK ? 1 : 4][STK ? 1 : NI];
     __shared__ uint32_t scb[4][NI];
     __shared__ double spr[4][NI];
     __shared__ uint8_t scert[4][NI][8];
@@ -1812,7 +1812,7 @@ void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_str
 }
 
 #ifndef FMRX_STICK_BPI
-#define FMRX_STICK_BPI 8  // batches an interval of the stick form: 128-step intervals (4: 64)
+#define FMRX_STICK_BPI 16  // batches an interval of the stick form: 256-step intervals (8: 128, 4: 64)
 #endif
 #ifndef FMRX_PIPE22_BPI
 #define FMRX_PIPE22_BPI 8  // batches an interval of the three-candidate form below the stick (128 steps)
