@@ -578,7 +578,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                                                       size_t ostride, int inject, int miss,
                                                       unsigned long long* stats, unsigned* redos) {
     constexpr int NI = NB * BPI;
-    static_assert(NI == 16 || NI == 32 || NI == 64 || (BPI > 1 && (NI == 128 || NI == 256 || (STK && NI == 512))),
+    static_assert(NI == 16 || NI == 32 || NI == 64 || (BPI > 1 && (NI == 128 || NI == 256)),
                   "the evaluators' lane map: 64 / NI lanes a step, or NI / 64 steps a lane");
     static_assert(NC == 3 || NC == 5, "three or five candidates");
     // STK: the stuck trigOffset (2^24, filter.cpp:165-166: 69.9 s into a stream).  Every step's
