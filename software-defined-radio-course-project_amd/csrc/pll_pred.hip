@@ -1815,7 +1815,7 @@ void launch_pll_pred(int waves, hipStream_t s, const float* io, int n, int n_str
 #define FMRX_STICK_BPI 16  // batches an interval of the stick form: 256-step intervals (8: 128, 4: 64)
 #endif
 #ifndef FMRX_PIPE22_BPI
-#define FMRX_PIPE22_BPI 8  // batches an interval of the three-candidate form below the stick (128 steps)
+#define FMRX_PIPE22_BPI 16  // batches an interval of the three-candidate form below the stick (256 steps)
 #endif
 #ifndef FMRX_PIPE21_BPI
 #define FMRX_PIPE21_BPI 8  // batches an interval of the five-candidate [2^21, 2^22) form (128 steps)
