@@ -1096,6 +1096,9 @@ int launch_pll_nco(float* io, int n, int n_streams, size_t stride, float nco_sca
     if (n <= 0) return 0;
     const size_t seg = pll_seg_len(n, n_streams);
     const float* args = reinterpret_cast<const float*>(side + 4 * seg * (size_t)n_streams);  // n per stream
+#ifdef FMRX_AB_NO_NCO
+    return 0;  // A/B build only (timing: what the NCO beside the chains costs them; output wrong)
+#endif
     hipLaunchKernelGGL(pll_nco_kernel, dim3((n + 255) / 256, n_streams), dim3(256), 0, s, io, n, stride, args,
                        (size_t)n, nco_scale, phase_adjust, st);
     return ok();
