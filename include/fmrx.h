@@ -264,7 +264,8 @@ int fmrx_debug_stage_timing(fmrx_ctx* ctx, int op, double* ms, double* steps, lo
 #define FMRX_KNOB_STEREO_HEAD 14      /* first chunk in 16ths of a chunk (8)          FMRX_STEREO_HEAD */
 #define FMRX_KNOB_STEREO_LEAD 15      /* n: chunk k's front end after chunk k-n's PLL  FMRX_STEREO_LEAD */
 #define FMRX_KNOB_AUDIO_DEFER 16      /* 0 beside the next PLL, 1 after the last, 2 (default) all but the
-                                         last chunk's beside the last PLL           FMRX_AUDIO_DEFER */
+                                         last chunk's beside the last PLL, 2 + e: the first e of
+                                         those beside the PLL before it             FMRX_AUDIO_DEFER */
 #define FMRX_KNOB_STEREO_TAIL 17      /* last chunk in 16ths of a chunk (8)          FMRX_STEREO_TAIL */
 int fmrx_debug_set_knob(fmrx_ctx* ctx, int knob, double value);
 

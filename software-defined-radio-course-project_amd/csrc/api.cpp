@@ -138,6 +138,7 @@ struct fmrx_ctx {
         int stereo_tail = 8;    // the last chunk's blocks in 16ths of a middle chunk's
         int stereo_lead = 0;    // n > 0: chunk k's front end waits for chunk k - n's PLL; 0: none
         int audio_defer = 2;    // 2: chunks 0 .. K-2's audio beside the last PLL; 1: all after it; 0: beside the next
+                                // (2 + e: chunks 0 .. e-1 beside the PLL before the last)
         int mono_split = -1;    // -1: kOlderShare; 0: equal spans; n: the older wave's n / 1024
         int bpf_tile = 1;       // 0: the per-output band-pass kernel
         int halo_kernel = 0;    // 1: the separate halo_kernel after the fused one
@@ -678,13 +679,18 @@ int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks,
         // chunk's after the last chunk's PLL (configs[4] 0.4168 -> 0.4113 s,
         // profiles/r05/ab_audio_defer/); 2, the default, chunks 0 .. K - 2 beside the LAST chunk's
         // PLL only and chunk K - 1's after it: a short tail, one chunk's chains disturbed
-        // (0.4058 -> 0.3955 s, profiles/r05/ab_audio_defer2/)
+        // (0.4058 -> 0.3955 s, profiles/r05/ab_audio_defer2/); 2 + e, chunks 0 .. e - 1 of those
+        // beside chunk K - 2's PLL instead (a shorter queue beside the last PLL)
         const int ad = c->knobs.audio_defer;
+        const int early = ad >= 2 ? std::min(ad - 2, K - 2) : 0;
         if (ad == 0 && (rc = audio(k))) return rc;
-        if (ad == 2 && k == K - 2)
-            for (int j = 0; j <= K - 2; j++)
+        if (ad >= 2 && early > 0 && k == K - 3)
+            for (int j = 0; j < early; j++)
                 if ((rc = audio(j))) return rc;
-        if (ad == 2 && k == K - 1 && (rc = audio(k))) return rc;
+        if (ad >= 2 && k == K - 2)
+            for (int j = early; j <= K - 2; j++)
+                if ((rc = audio(j))) return rc;
+        if (ad >= 2 && k == K - 1 && (rc = audio(k))) return rc;
     }
     if (c->knobs.audio_defer == 1)
         for (int j = 0; j < K; j++)
@@ -795,7 +801,7 @@ static fmrx_ctx::Knobs knobs_from_env() {
     k.stereo_head = std::max(1, get("FMRX_STEREO_HEAD", 8));
     k.stereo_tail = std::max(1, get("FMRX_STEREO_TAIL", 8));
     k.stereo_lead = std::max(0, get("FMRX_STEREO_LEAD", 0));
-    k.audio_defer = get("FMRX_AUDIO_DEFER", 2);
+    k.audio_defer = std::max(0, get("FMRX_AUDIO_DEFER", 2));
     k.mono_split = get("FMRX_MONO_SPLIT", -1);
     k.bpf_tile = get("FMRX_BPF_TILE", 1);
     k.halo_kernel = get("FMRX_HALO_KERNEL", 0);
@@ -1503,7 +1509,7 @@ int fmrx_debug_set_knob(fmrx_ctx* c, int knob, double value) {
         case FMRX_KNOB_STEREO_HEAD: k.stereo_head = std::max(1, v); break;
         case FMRX_KNOB_STEREO_TAIL: k.stereo_tail = std::max(1, v); break;
         case FMRX_KNOB_STEREO_LEAD: k.stereo_lead = std::max(0, v); break;
-        case FMRX_KNOB_AUDIO_DEFER: k.audio_defer = v; break;
+        case FMRX_KNOB_AUDIO_DEFER: k.audio_defer = std::max(0, v); break;
         case FMRX_KNOB_MONO_SPLIT: k.mono_split = v; break;
         case FMRX_KNOB_BPF_TILE: k.bpf_tile = v; break;
         case FMRX_KNOB_HALO_KERNEL: k.halo_kernel = v; break;

@@ -490,7 +490,9 @@ def test_stereo_multistream(fmrx, orc):
                                                            (2, 2, 3, "2", 0), (0, 70, 120, None, 0),
                                                            (0, 5, 48, "4", 1), (0, 70, 120, None, 2),
                                                            (0, 70, 120, None, -1), (1, 3, 40, "2", -1),
-                                                           (0, 70, 120, None, -2), (0, 5, 48, "4", -2)])
+                                                           (0, 70, 120, None, -2), (0, 5, 48, "4", -2),
+                                                           (0, 70, 120, None, -3), (0, 70, 120, None, -4),
+                                                           (0, 5, 48, "3", -4), (0, 5, 48, "2", -3)])
 def test_stereo_pipelined_chunks(fmrx, orc, monkeypatch, mode, n_streams, nb, chunks, lead):
     """The pipelined stereo engine (api.cpp run_stereo_pipelined): a call's blocks in chunks,
     front end + band-pass of chunk k + 1 and audio of chunk k - 1 on their own HIP streams beside
@@ -500,7 +502,8 @@ def test_stereo_pipelined_chunks(fmrx, orc, monkeypatch, mode, n_streams, nb, ch
     check the carried state.  Modes 0/1 take the tiled audio kernel, mode 2 the per-frame one.
     lead > 0: the paced schedule (chunk k's front end after chunk k - lead's PLL); lead <= 0: knob
     audio_defer = -lead (0 each chunk's audio beside the next PLL, 1 every chunk's after the last
-    PLL, 2 all but the last chunk's beside the last PLL)."""
+    PLL, 2 all but the last chunk's beside the last PLL, 2 + e the first e of those beside the PLL
+    before the last; e is clamped to K - 2, so 2 chunks with e = 1 is the plain 2 form)."""
     kw = {"stereo_lead": float(max(lead, 0)), "audio_defer": float(max(-lead, 0))}
     if chunks is not None:
         kw["stereo_chunks"] = float(chunks)
