@@ -85,6 +85,30 @@ FMRX_HD bool fast_sincos_f(float xf, float* s_out, float* c_out) {
     return s_ok && c_ok;
 }
 
+// The cosine alone (the NCO, filter.cpp:170): fast_sincos_f's reduction, kernels and bound, only
+// the cosine's rounding certified.  Where it returns true *c_out is float(cos(x)), the same float
+// fast_sincos_f or the library fallback gives.
+FMRX_HD bool fast_cos_f(float xf, float* c_out) {
+    const double x = (double)xf;
+    if (!(fabs(x) < 1.0e9) || !(fabs(x) > 1.0e-30)) return false;
+    const double nd = rint(x * kInvPio2);
+    const double r1 = fma(-nd, kPio2Hi, x);
+    const double r = fma(-nd, kPio2Lo, r1);
+    const double z = r * r;
+    const int q = (int)((long long)nd & 3);
+    double cv;
+    if (q & 1) {
+        const double ps = kS2 + z * (kS3 + z * (kS4 + z * (kS5 + z * kS6)));
+        const double sn = r + (z * r) * (kS1 + z * ps);
+        cv = q == 1 ? -sn : sn;
+    } else {
+        const double pc = z * (kC1 + z * (kC2 + z * (kC3 + z * (kC4 + z * (kC5 + z * kC6)))));
+        const double cs = 1.0 - (0.5 * z - z * pc);
+        cv = q == 0 ? cs : -cs;
+    }
+    return decide_float(cv, 1.5e-15 * fabs(cv) + fabs(nd) * 1.0e-32, c_out);
+}
+
 // fdlibm s_atan.c coefficients and breakpoints
 constexpr double kAtanHi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01,
                                9.82793723247329054082e-01, 1.57079632679489655800e+00};

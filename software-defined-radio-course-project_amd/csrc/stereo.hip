@@ -646,8 +646,13 @@ __global__ void pll_nco_kernel(float* io, int n, size_t stride, const float* arg
     if (i >= n) return;
     float* x = io + (size_t)s * stride;
     const float a = args[(size_t)s * astride + i] * nco_scale + phase_adjust;
-    float sv, cv;
+    float cv;
+#ifdef FMRX_AB_NCO_COS
+    if (!fast_cos_f(a, &cv)) cv = sincos_lib(a).y;  // A/B: only the cosine certified
+#else
+    float sv;
     if (!fast_sincos_f(a, &sv, &cv)) cv = sincos_lib(a).y;
+#endif
     x[i] = cv;
     if (i == n - 1) st[8 * (size_t)s + 4] = cv;
 }

@@ -58,6 +58,12 @@ int main(int argc, char** argv) {
                         } else {
                             c.fb++;
                         }
+                        // the cosine alone (fast_cos_f, the NCO): certified => glibc's float
+                        float c1;
+                        if (fmrx::fast_cos_f(x, &c1) && f2bits(c1) != f2bits((float)std::cos((double)x))) {
+                            if (c.bad < 5) std::printf("MISMATCH cos x=%.9g fast=%.9g\n", x, c1);
+                            c.bad++;
+                        }
                         // the PLL's own path (context-producing sincos, integer certification)
                         fmrx::PllCtx ctx{};
                         float s2, c2;
