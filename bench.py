@@ -153,7 +153,23 @@ def main() -> None:
                     help="configs[4] stream length (256 stereo streams sharded over the ranks)")
     ap.add_argument("--gather-chunks", type=int, default=4,
                     help="configs[4] at N > 1: time chunks whose PCM is gathered beside the next one's processing")
+    ap.add_argument("--repeats", type=int, default=5,
+                    help="timed repeats of configs[2] and configs[4] (median, min, max reported)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="the launch only: every rank joins the process group and rank 0 prints n_gpus (no GPU)")
     args = ap.parse_args()
+
+    # --gpus N means N GPUs: without a launcher's WORLD_SIZE, start N ranks under
+    # torch.distributed.run as a child process (nothing has touched the GPU yet) and exit with
+    # its status; under a launcher, its world size must be N
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(relaunch(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher's WORLD_SIZE is {env_world}", file=sys.stderr)
+        sys.exit(2)
+    if args.dry_run:
+        sys.exit(dry_run())
 
     import numpy as np
     import torch
@@ -306,14 +322,47 @@ def main() -> None:
         del d_iq, d_pcm
         rx.close()
         torch.cuda.empty_cache()
-        line["baseline_configs"] = other_configs(fmrx) if world == 1 else {}
-        c4 = streams_config(fmrx, world, rank, dev if world > 1 else 0, args.streams_seconds, args.gather_chunks)
+        line["baseline_configs"] = other_configs(fmrx, args.repeats) if world == 1 else {}
+        c4 = streams_config(fmrx, world, rank, dev if world > 1 else 0, args.streams_seconds, args.gather_chunks,
+                            args.repeats)
         if rank == 0:
             line["baseline_configs"]["configs[4]"] = c4
+            if world == 1 and not args.no_cpu_baseline and isinstance(c4, dict) and "error" not in c4:
+                c4["cpu_baseline"] = guarded(cpu_streams_baseline, fmrx, args.streams_seconds, c4)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def relaunch(n: int) -> int:
+    """bench.py --gpus n without a launcher: the same command as n ranks under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1), run as a child."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def dry_run() -> int:
+    """The launch alone (tests/test_bench_contract.py): every rank joins a gloo process group and
+    rank 0 prints the world size it would report as n_gpus."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world}), flush=True)
+    return 0
 
 
 # Serial-chain floors of the PLL runners (SURVEY §8d: the stereo configs are latency-bound), two
@@ -390,6 +439,26 @@ def cpu_reference_stereo(host_iq, gpu_pcm) -> dict:
     return out
 
 
+def cpu_baseline_stereo_stream(host_iq, h: dict, steps: int, sig: float) -> dict:
+    """The CPU baseline of one long stereo stream (tools/bench_unlocked.py: the PLL outside its
+    locked regime): the reference's stereo path (oracle/_ref, src/filter.cpp in project.cpp order,
+    1 core) on the same bytes, against the reference build's PCM hash of h (hashes.json)."""
+    import hashlib
+
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    if not oracle.reference_available():
+        return {"error": "oracle/_ref not built"}
+    t0 = time.perf_counter()
+    pcm = oracle.Reference().run(h["mode"], h["rf_taps"], host_iq, ["pcm"])["pcm"]
+    dt = time.perf_counter() - t0
+    return {"seconds": round(dt, 3), "cores": 1, "ns_per_pll_step": round(dt * 1e9 / steps, 1),
+            "x_realtime": round(sig / dt, 1), "kind": "reference",
+            "bit_exact": hashlib.sha256(pcm.tobytes()).hexdigest() == h["pcm_sha256"],
+            "sample": "the whole stream, oracle/_ref (src/filter.cpp in project.cpp order, whole chain)"}
+
+
 def threaded_project(exe, host_iq, gpu_pcm) -> dict:
     """The reference's two-thread `project 0 2` on the same bytes (stdin file -> stdout file)."""
     import subprocess
@@ -421,7 +490,7 @@ def guarded(fn, *args) -> dict:
         return {"error": repr(e)}
 
 
-def other_configs(fmrx) -> dict:
+def other_configs(fmrx, repeats: int = 5) -> dict:
     """The other single-GPU BASELINE configs, timed on the same box (extra keys; `value` stays
     configs[1]): configs[2] mode-0 stereo as ONE 1 GiB stream in one call (the serial PLL bounds
     it), configs[3] mode-2 mono (147/800 resampler) over 1 GiB, device-resident, synthetic."""
@@ -439,15 +508,20 @@ def other_configs(fmrx) -> dict:
         # scratch buffers; that allocation must not sit inside the timed call), then restart
         rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
         rx.synchronize()
-        rx.reset()
-        t0 = time.perf_counter()
-        rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
-        rx.synchronize()
-        dt = time.perf_counter() - t0
+        runs = []
+        for _ in range(max(1, repeats)):  # each timed call from the power-on state (fmrx_reset)
+            rx.reset()
+            rx.synchronize()
+            t0 = time.perf_counter()
+            rx.process_device(iq.data_ptr(), nb, pcm.data_ptr())
+            rx.synchronize()
+            runs.append(time.perf_counter() - t0)
+        dt = sorted(runs)[len(runs) // 2]
         sig = nb * bb / 2 / RT_RATE
         out["configs[2]"] = {"workload": f"mode-0 stereo (REF_EXACT), one stream, 1 GiB ({nb} blocks) in one call",
                              "seconds": round(dt, 3), "MS_per_s": round(nb * bb / 2 / dt / 1e6, 1),
-                             "x_realtime": round(sig / dt, 1)}
+                             "x_realtime": round(sig / dt, 1), "runs": [round(x, 4) for x in runs],
+                             "median": round(dt, 4), "min": round(min(runs), 4), "max": round(max(runs), 4)}
         par, host_iq, host_pcm = parity_vs_reference("bench_c2_m0_stereo_gib", iq, pcm, keep=True)
         out["configs[2]"].update(par)
         out["configs[2]"]["latency"] = stage_latency(rx, lambda: rx.process_device(iq.data_ptr(), nb, pcm.data_ptr()))
@@ -554,7 +628,8 @@ def parity_vs_reference(key: str, d_iq, d_pcm, keep: bool = False):
     return (res, h_iq, h_pcm) if keep else res
 
 
-def streams_config(fmrx, world: int, rank: int, dev: int, seconds: float, gather_chunks: int = 1) -> dict | None:
+def streams_config(fmrx, world: int, rank: int, dev: int, seconds: float, gather_chunks: int = 1,
+                   repeats: int = 5) -> dict | None:
     """BASELINE configs[4] at this N (extra key; `value` stays configs[1]): 256 independent
     mode-0 stereo streams of `seconds` each, sharded contiguously over the ranks (one process per
     GPU), each rank's shard one device-resident multi-stream call, the S16 PCM gathered to rank 0
@@ -570,11 +645,101 @@ def streams_config(fmrx, world: int, rank: int, dev: int, seconds: float, gather
     expect = iqgen.stream_hashes(256, int(seconds * geo.rf_fs * 2 // geo.block_bytes)) or None
     try:  # streams_leg agrees on failure across ranks before each collective (dist.run_leg)
         res = dmod.streams_leg(fmrx, 256, seconds, world, rank, dev, expect=expect, profile=stage_latency,
-                               gather_chunks=gather_chunks)
+                               gather_chunks=gather_chunks, repeats=repeats)
     except Exception as e:  # the headline line must still print
         res = {"error": repr(e)} if rank == 0 else None
     torch.cuda.empty_cache()
     return res
+
+
+def _stereo_worker(args):
+    """One host core: the reference's stereo path (oracle/_ref) over one configs[4] stream held in
+    shared memory (row k of n rows); returns its start / end time and PCM SHA-256."""
+    import hashlib
+    from multiprocessing import shared_memory
+
+    import numpy as np
+
+    shm_name, k, n_rows, row_bytes, barrier = args
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    ref = oracle.Reference()
+    shm = shared_memory.SharedMemory(name=shm_name)
+    try:
+        row = np.ndarray((n_rows, row_bytes), np.uint8, shm.buf)[k]
+        barrier.wait()
+        t0 = time.perf_counter()
+        pcm = ref.run(0, 51, row, ["pcm"])["pcm"]
+        t1 = time.perf_counter()
+        del row
+    finally:
+        shm.close()
+    return t0, t1, hashlib.sha256(pcm.tobytes()).hexdigest()
+
+
+def cpu_streams_baseline(fmrx, seconds: float, c4: dict) -> dict:
+    """configs[4]'s CPU baseline (SURVEY §8d ii): the reference's own stereo path (oracle/_ref,
+    src/filter.cpp in project.cpp order) with one stream per usable host core, all at once, on a
+    sample of the 256 streams spread over the ids, their PCM checked against the reference build's
+    hashes; the 256-stream time on those cores is extrapolated (ceil(256 / cores) rounds of the
+    measured wall)."""
+    import math
+    import multiprocessing as mp
+    from multiprocessing import shared_memory
+
+    import numpy as np
+    import torch
+
+    import iqgen
+
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    if not oracle.reference_available():
+        return {"error": "oracle/_ref not built"}
+    host = host_info()
+    cores = max(1, host["usable_cores"])
+    ids = [k * 256 // cores for k in range(cores)] if cores < 256 else list(range(256))
+    rx = fmrx.Receiver(0, fmrx.STEREO)
+    bb = rx.geo.block_bytes
+    nb = int(seconds * rx.geo.rf_fs * 2 // bb)
+    row_bytes = nb * bb
+    expect = iqgen.stream_hashes(256, nb)
+    shm = shared_memory.SharedMemory(create=True, size=len(ids) * row_bytes)
+    try:
+        rows = np.ndarray((len(ids), row_bytes), np.uint8, shm.buf)
+        d = torch.empty(row_bytes, dtype=torch.uint8, device="cuda")
+        for k, sid in enumerate(ids):  # the inputs, untimed (the same generator as the GPU leg's)
+            rx.synth_device(sid, 0, row_bytes // 2, d.data_ptr())
+            rx.synchronize()
+            rows[k] = d.cpu().numpy()
+        del d, rows
+        rx.close()
+        torch.cuda.empty_cache()
+        ctx = mp.get_context("spawn")
+        with ctx.Manager() as mgr:
+            barrier = mgr.Barrier(len(ids))
+            with ctx.Pool(len(ids)) as pool:
+                res = pool.map(_stereo_worker, [(shm.name, k, len(ids), row_bytes, barrier) for k in range(len(ids))])
+    finally:
+        shm.close()
+        shm.unlink()
+    wall = max(r[1] for r in res) - min(r[0] for r in res)
+    per = [r[1] - r[0] for r in res]
+    rounds = math.ceil(256 / len(ids))
+    est = wall * rounds
+    bad = [sid for sid, r in zip(ids, res) if expect.get(sid) is not None and r[2] != expect[sid]]
+    return {"value": round(len(ids) * nb * bb / 2 / wall / 1e6, 2), "unit": "MS/s", "cores": len(ids),
+            "kind": "reference", "streams_timed": ids,
+            "sample": f"{len(ids)} of the 256 streams x {seconds:g} s, one process per usable core, concurrently "
+                      "(oracle/_ref: src/filter.cpp in project.cpp order)",
+            "seconds_wall": round(wall, 3), "seconds_per_stream_mean": round(sum(per) / len(per), 3),
+            "seconds_256_streams_extrapolated": round(est, 2),
+            "extrapolation": f"ceil(256 / {len(ids)}) = {rounds} rounds of the measured wall on {len(ids)} cores",
+            "gpu_speedup_vs_extrapolated": round(est / c4["seconds"], 1) if c4.get("seconds") else None,
+            "bit_exact_vs_reference": not bad and all(expect.get(sid) for sid in ids),
+            "mismatched_streams": bad, "host": host}
 
 
 def cpu_baseline(d_iq, d_pcm, sample_bytes, bb, na):

@@ -221,11 +221,13 @@ int fmrx_debug_mono_stamps(fmrx_ctx* ctx, unsigned long long* d_stamps, size_t n
 int fmrx_debug_pll_stats(fmrx_ctx* ctx, unsigned long long* d_counts);
 
 /* ---- diagnostic: per-stream redos of the self-certifying PLL runners ----------------------- */
-/* With d_counts set (n_streams x 4 u32 on the device, zeroed and owned by the caller), the stereo *
- * calls add, per stream s, the intervals each self-certifying runner redid on the exact path      *
- * (a trigArg outside its candidates or an uncertified step) to d_counts[4 s + f]: f = 0 index     *
- * runner ([2^17, 2^20)), 1 three-wave 16-step form, 2 its 64-step five-candidate form, 3 the      *
- * three-candidate form.  Results are unchanged.  d_counts = NULL turns it off.                     */
+/* With d_counts set (n_streams x 8 u32 on the device, zeroed and owned by the caller), the stereo *
+ * calls and fmrx_pll (as stream 0) add, per stream s and trigOffset range r of a runner launch    *
+ * (r = 0 [2^17, 2^20), 1 [2^20, 2^21), 2 [2^21, 2^22), 3 from 2^22, the stuck 2^24 included):     *
+ * d_counts[8 s + r] += the intervals the runner redid on the exact path (a trigArg outside its    *
+ * candidates or an uncertified step), d_counts[8 s + 4 + r] += the steps it ran demoted (most of   *
+ * its last 32 intervals missed, as on an unlocked loop: the rest of the range on the exact path). *
+ * Results are unchanged.  d_counts = NULL turns it off.                                           */
 int fmrx_debug_pll_redos(fmrx_ctx* ctx, unsigned* d_counts);
 
 /* ---- diagnostic: per-stage device time of the stereo engine ------------------------------ */
@@ -246,27 +248,33 @@ int fmrx_debug_stage_timing(fmrx_ctx* ctx, int op, double* ms, double* steps, lo
  * measurements); a new context takes them from the environment variable named beside each
  * (read once, at fmrx_create).  The PLL test hooks make the runners do extra work that their
  * exact paths then redo (bit-identical output, counted by fmrx_debug_pll_stats); they are set
- * only here, never from the environment.  value: the knob's integer (the skew: samples).       */
-#define FMRX_KNOB_PLL_SPEC 0          /* 1 speculative runners, 0 the certified launch  FMRX_PLL_SPEC */
-#define FMRX_KNOB_PLL_SAT 1           /* 0: no saturated-segment runner                 FMRX_PLL_SAT  */
-#define FMRX_KNOB_PLL_PRED 2          /* 0 no predicted runners, 2 forced on            FMRX_PLL_PRED */
-#define FMRX_KNOB_PLL_PIPE 3          /* 0: no three-wave runner                        FMRX_PLL_PIPE */
-#define FMRX_KNOB_PLL_IDX 4           /* 2 index runner from 2^17, 1 from 2^18, 0 off  FMRX_PLL_IDX  */
-#define FMRX_KNOB_STEREO_CHUNKS 5     /* 0 auto, k chunks (1 the serial engine)   FMRX_STEREO_CHUNKS */
-#define FMRX_KNOB_MONO_SPLIT 6        /* -1 default, 0 equal, n/1024 older wave's    FMRX_MONO_SPLIT */
-#define FMRX_KNOB_BPF_TILE 7          /* 0: the per-output band-pass kernel             FMRX_BPF_TILE */
-#define FMRX_KNOB_HALO_KERNEL 8       /* 1: the separate halo kernel                 FMRX_HALO_KERNEL */
-#define FMRX_KNOB_PLL_INJECT 9        /* test hook: runners corrupt batch 1+(k+s)%(nb-1) of stream s  */
-#define FMRX_KNOB_PLL_PIPE_MISS 10    /* test hook: self-certifying runners miss interval k            */
-#define FMRX_KNOB_PLL_HINT_SKEW 11    /* test hook: host trigOffset bounds shifted by value samples    */
-#define FMRX_KNOB_PLL_CNT 12          /* bit f-17: count runner for form f's range (12)   FMRX_PLL_CNT  */
-#define FMRX_KNOB_PLL_STICK 13        /* 1: the stick form past trigOffset 2^24         FMRX_PLL_STICK */
-#define FMRX_KNOB_STEREO_HEAD 14      /* first chunk in 16ths of a chunk (8)          FMRX_STEREO_HEAD */
-#define FMRX_KNOB_STEREO_LEAD 15      /* n: chunk k's front end after chunk k-n's PLL  FMRX_STEREO_LEAD */
-#define FMRX_KNOB_AUDIO_DEFER 16      /* 0 beside the next PLL, 1 after the last, 2 (default) all but the
-                                         last chunk's beside the last PLL, 2 + e: the first e of
-                                         those beside the PLL before it             FMRX_AUDIO_DEFER */
-#define FMRX_KNOB_STEREO_TAIL 17      /* last chunk in 16ths of a chunk (8)          FMRX_STEREO_TAIL */
+ * only here, never from the environment.  value: the knob's integer (the skew: samples).
+ * Accepted range [lo, hi] in brackets: fmrx_debug_set_knob returns FMRX_EINVAL for a value
+ * outside it (or a fraction for an integer knob), fmrx_create for such an environment variable
+ * (tests/test_gpu_parity.py test_knob_sweep_bit_exact sweeps every value of every range).      */
+#define FMRX_KNOB_PLL_SPEC 0          /* [0,1] 1 speculative runners, 0 the certified launch FMRX_PLL_SPEC */
+#define FMRX_KNOB_PLL_SAT 1           /* [0,1] 0: no saturated-segment runner            FMRX_PLL_SAT  */
+#define FMRX_KNOB_PLL_PRED 2          /* [0,2] 0 no predicted runners, 2 forced on       FMRX_PLL_PRED */
+#define FMRX_KNOB_PLL_PIPE 3          /* [0,1] 0: no three-wave runner                   FMRX_PLL_PIPE */
+#define FMRX_KNOB_PLL_IDX 4           /* [0,2] 2 index runner from 2^17, 1 from 2^18, 0 off FMRX_PLL_IDX */
+#define FMRX_KNOB_STEREO_CHUNKS 5     /* [0,64] 0 auto, k chunks (1 the serial engine)  FMRX_STEREO_CHUNKS */
+#define FMRX_KNOB_MONO_SPLIT 6        /* [-1,1023] -1 default, 0 equal, n/1024 older wave's FMRX_MONO_SPLIT */
+#define FMRX_KNOB_BPF_TILE 7          /* [0,1] 0: the per-output band-pass kernel        FMRX_BPF_TILE */
+#define FMRX_KNOB_HALO_KERNEL 8       /* [0,1] 1: the separate halo kernel            FMRX_HALO_KERNEL */
+#define FMRX_KNOB_PLL_INJECT 9        /* [-1,2^30] test hook: runners corrupt batch 1+(k+s)%(nb-1) of stream s */
+#define FMRX_KNOB_PLL_PIPE_MISS 10    /* [-2^30,2^30] test hook: self-certifying runners miss interval k
+                                         (k >= 1), every interval from -k - 1 on (k <= -2: the demotion
+                                         runs), none (-1, 0)                                            */
+#define FMRX_KNOB_PLL_HINT_SKEW 11    /* [-2^24,2^24] test hook: host trigOffset bounds shifted by value */
+#define FMRX_KNOB_PLL_CNT 12          /* [0,31] bit f-17: count runner for form f's range (12) FMRX_PLL_CNT */
+#define FMRX_KNOB_PLL_STICK 13        /* [0,1] 1: the stick form past trigOffset 2^24    FMRX_PLL_STICK */
+#define FMRX_KNOB_STEREO_HEAD 14      /* [1,64] first chunk in 16ths of a chunk (8)    FMRX_STEREO_HEAD */
+#define FMRX_KNOB_STEREO_LEAD 15      /* [0,64] n: chunk k's front end after chunk k-n's PLL FMRX_STEREO_LEAD */
+#define FMRX_KNOB_AUDIO_DEFER 16      /* [0,64] 0 beside the next PLL, 1 after the last, 2 (default) all but
+                                         the last chunk's beside the last PLL, 2 + e: the first e of those
+                                         beside the PLL before it (e past the chunks: all of them)
+                                                                                     FMRX_AUDIO_DEFER */
+#define FMRX_KNOB_STEREO_TAIL 17      /* [1,64] last chunk in 16ths of a chunk (8)     FMRX_STEREO_TAIL */
 int fmrx_debug_set_knob(fmrx_ctx* ctx, int knob, double value);
 
 #ifdef __cplusplus

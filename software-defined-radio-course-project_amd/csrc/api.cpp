@@ -784,28 +784,88 @@ int fmrx_geometry(const fmrx_config* cfg, fmrx_geometry_t* g) {
 // The tuning switches of a new context from the environment (A/B measurements: which runner or
 // kernel form runs, never what it computes).  The PLL test hooks are not read here: only
 // fmrx_debug_set_knob sets them, per context.
-static fmrx_ctx::Knobs knobs_from_env() {
+// Every knob's accepted range (include/fmrx.h): a value outside it is refused (FMRX_EINVAL from
+// fmrx_debug_set_knob; fmrx_create refuses a bad environment variable), so no setting can reach
+// an untested kernel form.  Integer knobs take integer values only.
+struct KnobSpec {
+    int id;
+    const char* env;  // the tuning knobs' environment variable (null: test hooks, never from there)
+    double lo, hi;
+    bool integer;
+};
+constexpr KnobSpec kKnobs[] = {
+    {FMRX_KNOB_PLL_SPEC, "FMRX_PLL_SPEC", 0, 1, true},
+    {FMRX_KNOB_PLL_SAT, "FMRX_PLL_SAT", 0, 1, true},
+    {FMRX_KNOB_PLL_PRED, "FMRX_PLL_PRED", 0, 2, true},
+    {FMRX_KNOB_PLL_PIPE, "FMRX_PLL_PIPE", 0, 1, true},
+    {FMRX_KNOB_PLL_IDX, "FMRX_PLL_IDX", 0, 2, true},
+    {FMRX_KNOB_STEREO_CHUNKS, "FMRX_STEREO_CHUNKS", 0, 64, true},
+    {FMRX_KNOB_MONO_SPLIT, "FMRX_MONO_SPLIT", -1, 1023, true},
+    {FMRX_KNOB_BPF_TILE, "FMRX_BPF_TILE", 0, 1, true},
+    {FMRX_KNOB_HALO_KERNEL, "FMRX_HALO_KERNEL", 0, 1, true},
+    {FMRX_KNOB_PLL_INJECT, nullptr, -1, 1 << 30, true},
+    {FMRX_KNOB_PLL_PIPE_MISS, nullptr, -(1 << 30), 1 << 30, true},
+    {FMRX_KNOB_PLL_HINT_SKEW, nullptr, -16777216.0, 16777216.0, false},
+    {FMRX_KNOB_PLL_CNT, "FMRX_PLL_CNT", 0, 31, true},
+    {FMRX_KNOB_PLL_STICK, "FMRX_PLL_STICK", 0, 1, true},
+    {FMRX_KNOB_STEREO_HEAD, "FMRX_STEREO_HEAD", 1, 64, true},
+    {FMRX_KNOB_STEREO_LEAD, "FMRX_STEREO_LEAD", 0, 64, true},
+    {FMRX_KNOB_AUDIO_DEFER, "FMRX_AUDIO_DEFER", 0, 64, true},
+    {FMRX_KNOB_STEREO_TAIL, "FMRX_STEREO_TAIL", 1, 64, true},
+};
+
+const KnobSpec* knob_spec(int knob) {
+    for (const KnobSpec& k : kKnobs)
+        if (k.id == knob) return &k;
+    return nullptr;
+}
+
+// value into the context's knobs (range already checked)
+void knob_set(fmrx_ctx::Knobs& k, int knob, double value) {
+    const int v = (int)value;
+    switch (knob) {
+        case FMRX_KNOB_PLL_SPEC: k.pll.spec = v; break;
+        case FMRX_KNOB_PLL_SAT: k.pll.sat = v; break;
+        case FMRX_KNOB_PLL_PRED: k.pll.pred = v; break;
+        case FMRX_KNOB_PLL_PIPE: k.pll.pipe = v; break;
+        case FMRX_KNOB_PLL_IDX: k.pll.idx = v; break;
+        case FMRX_KNOB_STEREO_CHUNKS: k.stereo_chunks = v; break;
+        case FMRX_KNOB_STEREO_HEAD: k.stereo_head = v; break;
+        case FMRX_KNOB_STEREO_TAIL: k.stereo_tail = v; break;
+        case FMRX_KNOB_STEREO_LEAD: k.stereo_lead = v; break;
+        case FMRX_KNOB_AUDIO_DEFER: k.audio_defer = v; break;
+        case FMRX_KNOB_MONO_SPLIT: k.mono_split = v; break;
+        case FMRX_KNOB_BPF_TILE: k.bpf_tile = v; break;
+        case FMRX_KNOB_HALO_KERNEL: k.halo_kernel = v; break;
+        case FMRX_KNOB_PLL_INJECT: k.pll.inject = v; break;
+        case FMRX_KNOB_PLL_PIPE_MISS: k.pll.pipe_miss = v; break;
+        case FMRX_KNOB_PLL_HINT_SKEW: k.pll.skew = value; break;
+        case FMRX_KNOB_PLL_CNT: k.pll.cnt = v; break;
+        case FMRX_KNOB_PLL_STICK: k.pll.stick = v; break;
+        default: break;
+    }
+}
+
+bool knob_ok(const KnobSpec& s, double v) {
+    return v == v && v >= s.lo && v <= s.hi && (!s.integer || v == std::floor(v));
+}
+
+// the tuning knobs from the environment, read once by fmrx_create; a set variable must be an
+// integer in its knob's range (otherwise the context is refused, naming the variable)
+int knobs_from_env(fmrx_ctx::Knobs* out) {
     fmrx_ctx::Knobs k;
-    auto get = [](const char* name, int def) {
-        const char* e = std::getenv(name);
-        return (e && *e) ? std::atoi(e) : def;
-    };
-    k.pll.spec = get("FMRX_PLL_SPEC", 1);
-    k.pll.sat = get("FMRX_PLL_SAT", 1);
-    k.pll.pred = get("FMRX_PLL_PRED", 1);
-    k.pll.pipe = get("FMRX_PLL_PIPE", 1);
-    k.pll.idx = get("FMRX_PLL_IDX", 2);
-    k.pll.cnt = get("FMRX_PLL_CNT", kPllCntDefault);
-    k.pll.stick = get("FMRX_PLL_STICK", 1);
-    k.stereo_chunks = std::max(0, get("FMRX_STEREO_CHUNKS", 0));
-    k.stereo_head = std::max(1, get("FMRX_STEREO_HEAD", 8));
-    k.stereo_tail = std::max(1, get("FMRX_STEREO_TAIL", 8));
-    k.stereo_lead = std::max(0, get("FMRX_STEREO_LEAD", 0));
-    k.audio_defer = std::max(0, get("FMRX_AUDIO_DEFER", 2));
-    k.mono_split = get("FMRX_MONO_SPLIT", -1);
-    k.bpf_tile = get("FMRX_BPF_TILE", 1);
-    k.halo_kernel = get("FMRX_HALO_KERNEL", 0);
-    return k;
+    for (const KnobSpec& s : kKnobs) {
+        if (!s.env) continue;
+        const char* e = std::getenv(s.env);
+        if (!e || !*e) continue;
+        char* end = nullptr;
+        const long v = std::strtol(e, &end, 10);
+        if (*end != '\0' || !knob_ok(s, (double)v))
+            return fail(FMRX_EINVAL, "%s=%s: not an integer in [%g, %g]", s.env, e, s.lo, s.hi);
+        knob_set(k, s.id, (double)v);
+    }
+    *out = k;
+    return FMRX_OK;
 }
 
 int fmrx_create(const fmrx_config* cfg, fmrx_ctx** out) {
@@ -838,7 +898,10 @@ int fmrx_create(const fmrx_config* cfg, fmrx_ctx** out) {
                     g.rf_decim);
     }
     if ((rc = set_device(c))) { delete c; return rc; }
-    c->knobs = knobs_from_env();
+    if ((rc = knobs_from_env(&c->knobs))) {
+        delete c;
+        return rc;
+    }
     {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess && cus > 0)
@@ -1348,6 +1411,7 @@ int fmrx_pll(fmrx_ctx* c, float* d_io, int n, float freq, float fs, float nco_sc
     hint.known = trig >= 0.0f && trig <= 16777216.0f && trig == std::floor(trig);
     hint.trig_lo = hint.trig_hi = hint.known ? (double)trig : 0.0;
     hint.timer = c->stage_timer.on ? &c->stage_timer : nullptr;
+    hint.redos = c->pll_redos;  // fmrx_debug_pll_redos: as stream 0
     if (launch_pll(d_io, n, 1, (size_t)n, freq, fs, nco_scale, phase_adjust, norm_bw, c->d_scratch.p,
                    c->d_pll_side.p, c->stream, hint, c->pll_stats))
         return fail(FMRX_EHIP, "launch failed");
@@ -1497,29 +1561,10 @@ int fmrx_debug_stage_timing(fmrx_ctx* c, int op, double* ms, double* steps, long
 int fmrx_debug_set_knob(fmrx_ctx* c, int knob, double value) {
     CtxLock lock_(c);
     if (!c) return fail(FMRX_EINVAL, "null context");
-    fmrx_ctx::Knobs& k = c->knobs;
-    const int v = (int)value;
-    switch (knob) {
-        case FMRX_KNOB_PLL_SPEC: k.pll.spec = v; break;
-        case FMRX_KNOB_PLL_SAT: k.pll.sat = v; break;
-        case FMRX_KNOB_PLL_PRED: k.pll.pred = v; break;
-        case FMRX_KNOB_PLL_PIPE: k.pll.pipe = v; break;
-        case FMRX_KNOB_PLL_IDX: k.pll.idx = v; break;
-        case FMRX_KNOB_STEREO_CHUNKS: k.stereo_chunks = std::max(0, v); break;
-        case FMRX_KNOB_STEREO_HEAD: k.stereo_head = std::max(1, v); break;
-        case FMRX_KNOB_STEREO_TAIL: k.stereo_tail = std::max(1, v); break;
-        case FMRX_KNOB_STEREO_LEAD: k.stereo_lead = std::max(0, v); break;
-        case FMRX_KNOB_AUDIO_DEFER: k.audio_defer = std::max(0, v); break;
-        case FMRX_KNOB_MONO_SPLIT: k.mono_split = v; break;
-        case FMRX_KNOB_BPF_TILE: k.bpf_tile = v; break;
-        case FMRX_KNOB_HALO_KERNEL: k.halo_kernel = v; break;
-        case FMRX_KNOB_PLL_INJECT: k.pll.inject = v; break;
-        case FMRX_KNOB_PLL_PIPE_MISS: k.pll.pipe_miss = v; break;
-        case FMRX_KNOB_PLL_HINT_SKEW: k.pll.skew = value; break;
-        case FMRX_KNOB_PLL_CNT: k.pll.cnt = v; break;
-        case FMRX_KNOB_PLL_STICK: k.pll.stick = v; break;
-        default: return fail(FMRX_EINVAL, "unknown knob %d", knob);
-    }
+    const KnobSpec* s = knob_spec(knob);
+    if (!s) return fail(FMRX_EINVAL, "unknown knob %d", knob);
+    if (!knob_ok(*s, value)) return fail(FMRX_EINVAL, "knob %d: %g outside [%g, %g]", knob, value, s->lo, s->hi);
+    knob_set(c->knobs, knob, value);
     return FMRX_OK;
 }
 

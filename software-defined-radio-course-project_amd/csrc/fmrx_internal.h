@@ -99,6 +99,13 @@ struct StageTimer {
     }
 };
 
+// The count runner's forms by default: [2^19, 2^20) and [2^20, 2^21) (bits 2, 3).  Same-box A/B,
+// two alternating rounds (profiles/r05/ab_cnt12/): one 10 s stream 0.1093 -> 0.0923 s, configs[4]
+// 0.430 -> 0.418 s, configs[2] 1.240 -> 1.222 s.  [2^17, 2^19) stay on the index runner (the
+// count form's 31-candidate evaluators bound it: 68-73 ns a step against 55), [2^21, 2^22) on the
+// three-wave runner (profiles/r05/rprof/).
+constexpr int kPllCntDefault = 12;
+
 // Per-context switches of the PLL launch (api.cpp fmrx_ctx::knobs; fmrx_debug_set_knob).  The
 // tuning ones pick which runners run (same bits either way) and are read from the environment
 // once, when the context is created; the test hooks make the runners do extra (redone) work --
@@ -109,7 +116,7 @@ struct PllKnobs {
     int pred = 1;        // 0: no predicted runners; 2: the two-wave one even where waves share SIMDs
     int pipe = 1;        // 0: no three-wave runner (FMRX_PLL_PIPE)
     int idx = 2;         // index runner from 2^17 (2), from 2^18 (1), off (0) (FMRX_PLL_IDX)
-    int cnt = 12;        // bit f - 17: the count runner takes form f's range (FMRX_PLL_CNT; kPllCntDefault)
+    int cnt = kPllCntDefault;  // bit f - 17: the count runner takes form f's range (FMRX_PLL_CNT)
     int stick = 1;       // the three-candidate runner's stick form past trigOffset 2^24 (FMRX_PLL_STICK)
     int inject = -1;     // test hook: the runners corrupt batch 1 + (k + s) % (nb - 1) of stream s
     int pipe_miss = -1;  // test hook: the self-certifying runners report interval k as missed
@@ -118,7 +125,7 @@ struct PllKnobs {
 struct PllHint {
     int n_simd = 1024;
     PllKnobs knobs;
-    unsigned* redos = nullptr;  // fmrx_debug_pll_redos (diagnostic): n_streams x kPllRedoForms
+    unsigned* redos = nullptr;  // fmrx_debug_pll_redos (diagnostic): n_streams x kPllRedoSlots
     bool known = false;
     double trig_lo = 0.0, trig_hi = 0.0;
     StageTimer* timer = nullptr;  // diagnostic stage timing (null: off)
@@ -173,15 +180,19 @@ int launch_pll_idx(hipStream_t s, const float* io, int n, int n_streams, size_t 
 int launch_pll_cnt(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
                    float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats,
                    unsigned* redos = nullptr);
-// The count runner's forms by default: [2^19, 2^20) and [2^20, 2^21) (bits 2, 3).  Same-box A/B,
-// two alternating rounds (profiles/r05/ab_cnt12/): one 10 s stream 0.1093 -> 0.0923 s, configs[4]
-// 0.430 -> 0.418 s, configs[2] 1.240 -> 1.222 s.  [2^17, 2^19) stay on the index runner (the
-// count form's 31-candidate evaluators bound it: 68-73 ns a step against 55), [2^21, 2^22) on the
-// three-wave runner (profiles/r05/rprof/).
-constexpr int kPllCntDefault = 12;
-// fmrx_debug_pll_redos: per stream, intervals the self-certifying runners redid, by form (0 index,
-// 1 three-wave 16-step, 2 three-wave 64-step five candidates, 3 three candidates)
-constexpr int kPllRedoForms = 4;
+// pll_demote.hip: the rest of a self-certifying runner launch's range for the streams it demoted
+// (pll_device.h pll_demote): the same arguments as the runner launch it follows on stream s.  That
+// launch leaves each stream's first step for this kernel in the PLL state's slot 6 (int bits; 0:
+// not demoted), which this kernel clears.  One stream a workgroup: a speculative chain
+// (pll_spec_lane_kernel's step) checked a sub-segment behind by the other waves, which also form
+// its side data; a batch that does not verify is recomputed exactly and the chain resumes after it.
+int launch_pll_demoted(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step,
+                       float norm_bw, float* st, float* out, size_t ostride, int inject, unsigned long long* stats);
+// fmrx_debug_pll_redos: per stream kPllRedoSlots u32, by the trigOffset range r of the runner's
+// launch (0 [2^17, 2^20), 1 [2^20, 2^21), 2 [2^21, 2^22), 3 from 2^22, the stick included):
+// slot r the intervals the self-certifying runners redid exactly, slot 4 + r the steps they ran
+// demoted (pll_demote: the rest of a range on the exact path after most intervals missed)
+constexpr int kPllRedoSlots = 8;
 constexpr int kPllIdxSimds = 4;  // SIMDs a stream takes: one CU (launch_pll admits n_simd / 4 streams)
 // the index runner's lowest trigOffset: 2^17 (kPllIdxMin64; 2^18, kPllIdxMin, with FMRX_PLL_IDX=1).  In
 // [2^17, 2^18) 32 candidates (c0 - 16 .. c0 + 15) run 62 ns a step with their misses redone,

@@ -72,6 +72,24 @@ __device__ __noinline__ PllPair pll_redo(PllState p, PllCtx ctx, const float* xb
 // certification is ~23 % of the step: without it the loop runs 0.31 s instead of 0.40 s.
 constexpr int kPllBatch = 16;
 
+// Demotion of a self-certifying runner's stream (pll_pred.hip): the chain keeps the verdicts of
+// its last 32 intervals as bits; past kPllDemoteMisses misses among them the trigArgs are not
+// where the candidates are predicted (an unlocked loop: no pilot, noise, mode 2/3's if_fs, whose
+// phase moves many candidate cells an interval) and the runner leaves the rest of its range to
+// pll_demoted_kernel (pll_demote.hip: a speculative chain checked behind it, ~lane-runner speed)
+// instead of paying a failed interval plus its redo each time.  Locked streams miss <= ~1 % of
+// intervals (profiles/r05 redos); unlocked ones 75-100 % (profiles/r06/unlocked.json).
+constexpr int kPllDemoteMisses = 24;
+// test hook (knob pll_pipe_miss = m): m >= 1 a forced miss on interval m (past the last: the last),
+// m <= -2 on every interval from -m - 1 on (an unlocked loop's pattern: the demotion runs), -1 off
+__device__ inline bool pll_hook_miss(int i, int miss, int ni) {
+    return miss >= 1 ? i == min(miss, ni) : (miss <= -2 && i >= -miss - 1);
+}
+__device__ inline bool pll_demote(uint32_t& hist, bool miss) {
+    hist = (hist << 1) | (miss ? 1u : 0u);
+    return __builtin_popcount(hist) >= kPllDemoteMisses;
+}
+
 template <int L>
 __device__ inline double row_bcast(double v) {
     const long long bits = __builtin_bit_cast(long long, v);
@@ -117,6 +135,12 @@ constexpr float kPllPipeMinLow = 1048576.0f;  // 2^20
 __device__ inline bool pll_pipe_stream(float trig0, double step, float lo = kPllPipeMinLow,
                                        float hi = kPllTrigStick) {
     return trig0 >= lo && trig0 <= hi && trig0 == floorf(trig0) && fabs(step * (double)kPllTrigStick) < kPllMaxPr;
+}
+
+// the fmrx_debug_pll_redos slot of a runner launch whose range starts at trigOffset t0
+// (fmrx_internal.h kPllRedoSlots)
+__device__ inline int pll_redo_range(float t0) {
+    return t0 < kPllPipeMinLow ? 0 : t0 < kPllPipeMin5 ? 1 : t0 < kPllPipeMin ? 2 : 3;
 }
 
 }  // namespace

@@ -614,6 +614,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     constexpr bool REPLAY = BPI > 1;
     __shared__ float sph[REPLAY ? 1 : 4][REPLAY ? 1 : NI];
     __shared__ int smiss[4], sexact[4];
+    __shared__ int sdemote;  // the chain demoted the stream (pll_demote) at its redo
     __shared__ __attribute__((aligned(16))) float sek[STK ? 4 : 1][STK ? 3 * NI : 4];
     __shared__ float2 sthr[4];
     // the candidate data the chain and the replay select from at step J of ring slot sl: (T0, T1,
@@ -675,6 +676,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             exact(p, c, 0, n);
             if (t == 0) {
                 S[0] = p.integ; S[1] = p.phase; S[2] = p.fbI; S[3] = p.fbQ; S[5] = p.trig;
+                S[6] = 0.0f;  // not demoted (pll_demoted_kernel)
                 if (stats) {  // outside the domain: the whole range "resumed" on the exact path
                     if (!in_domain) atomicAdd(stats, (unsigned long long)nb);
                     atomicAdd(stats + 1, (unsigned long long)nb);
@@ -779,7 +781,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 // pll_batch_fast's range test, on the state at the batch's start
                 const float2 r0 = sst[(k - 1) & 3][BPI - 1];
                 const bool bad = verdict(sl, l, a) || !(fabsf(r0.y) < kPllMaxPhase && fabsf(r0.x) < kPllMaxInteg);
-                const bool any = __builtin_amdgcn_ballot_w64(h == 0 && bad) != 0 || k == min(miss, ni);
+                const bool any = __builtin_amdgcn_ballot_w64(h == 0 && bad) != 0 || pll_hook_miss(k, miss, ni);
                 // test hooks: a forced miss (the redo path); inject's is counted as resumed
                 if (t == 0) smiss[sl] = k == inj ? 2 : any ? 1 : 0;
                 return;
@@ -857,7 +859,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 if (act) out[j0(k) + J] = a;
                 anybad = anybad || (act && bad);
             }
-            const bool any = __builtin_amdgcn_ballot_w64(anybad) != 0 || k == min(miss, ni);
+            const bool any = __builtin_amdgcn_ballot_w64(anybad) != 0 || pll_hook_miss(k, miss, ni);
             // test hooks: a forced miss (the redo path); inject's is counted as resumed
             if (t == 0) smiss[sl] = k == inj ? 2 : any ? 1 : 0;
         };
@@ -867,15 +869,17 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         ld(1 + RD, vq[1 % RD]);
         __syncthreads();  // (prologue)
         unsigned long long ev_body = 0, ev_wait = 0, ev_put = 0, ev_check = 0;
+        // the chain demoted the stream at a redo (pll_demote): it runs the rest of the range alone
+        bool demoted = false;
         // interval i: interval i + 1's data, interval i - 1's check; groups of RD intervals from
         // i0 = 1 (mod RD), so the ring slots are compile-time
-        for (int i0 = 1; i0 <= ni; i0 += RD) {
+        for (int i0 = 1; i0 <= ni && !demoted; i0 += RD) {
             unroll_ic(
                 [&](auto uc) {
                     constexpr int u = decltype(uc)::value;
                     constexpr int sl = (2 + u) % RD;  // slot of interval i + 1
                     const int i = i0 + u;
-                    if (i <= ni) {
+                    if (i <= ni && !demoted) {
                         const unsigned long long p0 = PROF_T();
                         if (i + 1 <= ni) {
                             put(i + 1, sst[(i - 1) & 3][BPI - 1].y, vq[sl]);
@@ -892,6 +896,10 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                             // and i on candidates predicted anew here from the corrected phase
                             __syncthreads();  // B1: the chain's exact redo of i - 2 follows
                             __syncthreads();  // B1.5: i - 2's exact end state is in the ring
+                            if (__builtin_amdgcn_readfirstlane(sdemote)) {  // set before B1.5
+                                demoted = true;
+                                return;
+                            }
                             {
                                 float v[SPL];
                                 ld(i, v);
@@ -914,8 +922,10 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                 },
                 std::make_integer_sequence<int, RD>{});
         }
-        check(ni);
-        __syncthreads();  // the chain reads the last two verdicts
+        if (!demoted) {
+            check(ni);
+            __syncthreads();  // the chain reads the last two verdicts
+        }
 #ifdef FMRX_AB_PROF
         if (t == 0 && w == 1) {
             atomicAdd(&g_pipe_prof[2], ev_body);
@@ -961,9 +971,15 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             smiss[k] = 0;
             sexact[k] = k == 0;
         }
+        sdemote = 0;
     }
     __syncthreads();  // (prologue)
-    unsigned long long ch_body = 0, ch_wait = 0, n_redo = 0, n_inj = 0;
+    unsigned long long ch_body = 0, ch_wait = 0, n_redo = 0, n_inj = 0, n_dem = 0;
+    uint32_t hist = 0;  // the last 32 verdicts (pll_demote)
+    bool demoted = false;
+    PllState qd;        // demoted: the exact state at the end of the redone interval, and its step
+    PllCtx cd{};
+    long long jd = 0;
     // interval i on the fast chain from (integ, phase) and the carry, its data in ring slot i & 3
     auto run = [&](int i) {
         const int is = i & 3;
@@ -1057,6 +1073,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         const unsigned long long p0 = PROF_T();
         const int flag = smiss[(i - 2) & 3];  // the verdict on interval i - 2 (slot 3 is clear at i = 1)
         run(i);
+        const bool over = pll_demote(hist, __builtin_amdgcn_readfirstlane(flag) != 0);
         if (__builtin_amdgcn_readfirstlane(flag)) {
             n_redo++;
             n_inj += inj == i - 2 ? 1 : 0;  // the inject hook's interval, redone exactly
@@ -1077,6 +1094,15 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             }
             integ = q.integ;
             phase = q.phase;
+            if (over) {  // demoted: the evaluators leave after B1.5, pll_demoted_kernel runs the rest
+                sdemote = 1;
+                __syncthreads();  // B1.5
+                demoted = true;
+                qd = q;
+                cd = c;
+                jd = j0(f) + NI;
+                break;
+            }
             carry_exact((float)c.x, f + 1);
             __syncthreads();  // B1.5: the evaluators predict interval i anew from i - 2's end
             // interval i - 1 again on the fast chain: its candidates came from the phase at the
@@ -1092,19 +1118,28 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         ch_body += p1 - p0;
         ch_wait += PROF_T() - p1;
     }
-    __syncthreads();  // E2's checks of the last two intervals
-    // a miss in them: from the first missed interval on exactly; then the steps past the last
-    // interval exactly, from the state at the end of the last good interval
-    const int f = smiss[(ni - 1) & 3] ? ni - 1 : (smiss[ni & 3] ? ni : ni + 1);
-    const float2 r0 = sst[(f - 1) & 3][BPI - 1];
-    const long long jf = j0(f);
-    const float a = (float)(pr_at(jf - 1) + (double)r0.y);
     PllState q;
     PllCtx c{};
-    pll_state_at(q, c, r0.x, r0.y, trig0, jf, a, DeviceLib{});
-    exact(q, c, jf, n);
+    int f;  // the first interval the tail below runs exactly
+    if (demoted) {  // the redone interval's exact end: pll_demoted_kernel runs the rest
+        q = qd;
+        c = cd;
+        f = (int)((jd - NB) / NI) + 1;
+        n_dem = (unsigned long long)(n - jd);
+    } else {
+        __syncthreads();  // E2's checks of the last two intervals
+        // a miss in them: from the first missed interval on exactly; then the steps past the last
+        // interval exactly, from the state at the end of the last good interval
+        f = smiss[(ni - 1) & 3] ? ni - 1 : (smiss[ni & 3] ? ni : ni + 1);
+        const float2 r0 = sst[(f - 1) & 3][BPI - 1];
+        const long long jf = j0(f);
+        const float a = (float)(pr_at(jf - 1) + (double)r0.y);
+        pll_state_at(q, c, r0.x, r0.y, trig0, jf, a, DeviceLib{});
+        exact(q, c, jf, n);
+    }
     if (t == 0) {
         S[0] = q.integ; S[1] = q.phase; S[2] = q.fbI; S[3] = q.fbQ; S[5] = q.trig;
+        S[6] = __builtin_bit_cast(float, demoted ? (int)jd : 0);  // pll_demoted_kernel's first step, or 0
         // fmrx_debug_pll_stats: batches run; "resumed" only for the inject hook's forced redos
         // (the runner is exact by construction: its own redos of missed intervals are internal)
         if (stats) {
@@ -1112,9 +1147,13 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             atomicAdd(stats, (n_inj + (unsigned long long)fin) * 3 * BPI);
             atomicAdd(stats + 1, (unsigned long long)nb);
         }
-        // fmrx_debug_pll_redos: this stream's redone intervals, by form (1: 16-step five
-        // candidates, 2: 64-step five, 3: three)
-        if (redos) atomicAdd(&redos[kPllRedoForms * (size_t)s + (NI == 16 ? 1 : NC == 5 ? 2 : 3)], (unsigned)n_redo);
+        // fmrx_debug_pll_redos: this stream's redone intervals and demoted steps
+        if (redos) {  // by the range's trigOffset (1: the 16-step five-candidate form, 2: the 64/128-step
+                      // one, 3: three candidates and the stick)
+            const int rg = NI == 16 ? 1 : NC == 5 ? 2 : 3;
+            atomicAdd(&redos[kPllRedoSlots * (size_t)s + rg], (unsigned)n_redo);
+            atomicAdd(&redos[kPllRedoSlots * (size_t)s + 4 + rg], (unsigned)n_dem);
+        }
     }
 #ifdef FMRX_AB_PROF
     if (t == 0) {
@@ -1131,6 +1170,14 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     (void)n_inj;
 }
 
+
+// A/B build only (make ab AB=-DFMRX_AB_NODEMOTE): the index and count runners without pll_demote's
+// checks (timing of the locked path; an unlocked stream then redoes every interval)
+#ifdef FMRX_AB_NODEMOTE
+constexpr bool kAbNoDemote = true;
+#else
+constexpr bool kAbNoDemote = false;
+#endif
 
 // ---- pll_idx_kernel: one stream a workgroup of 1 + NW waves, trigOffset in [2^17, 2^20) ---------
 //
@@ -1180,6 +1227,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
     __shared__ int srow[4][NI];
     __shared__ float2 sst[4];
     __shared__ int sexact[4];
+    __shared__ int sdemote;  // the interval after which the chain left (pll_demote), or 0
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
     const int s = blockIdx.x;  // grid = n_streams
     const float* x = io + (size_t)s * stride;
@@ -1213,6 +1261,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
             exact(p, c, 0, n);
             if (t == 0) {
                 S[0] = p.integ; S[1] = p.phase; S[2] = p.fbI; S[3] = p.fbQ; S[5] = p.trig;
+                S[6] = 0.0f;  // not demoted (pll_demoted_kernel)
                 if (stats) {
                     if (!in_domain) atomicAdd(stats, (unsigned long long)nb);
                     atomicAdd(stats + 1, (unsigned long long)nb);
@@ -1276,13 +1325,27 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         ld(1 + RD, vq[1 % RD]);
         __syncthreads();  // (prologue)
         unsigned long long ev_body = 0, ev_wait = 0;
-        for (int i0 = 1; i0 <= ni; i0 += RD) {
+        // the chain demoted the stream (pll_demote) after redoing interval i - 1 itself: it runs the
+        // rest of the range alone, no barrier is reached any more
+        bool demoted = false;
+        for (int i0 = 1; i0 <= ni && !demoted; i0 += RD) {
             unroll_ic(
                 [&](auto uc) {
                     constexpr int u = decltype(uc)::value;
                     constexpr int sl = (2 + u) % RD;  // slot of interval i + 1
                     const int i = i0 + u;
-                    if (i <= ni) {
+                    if (i <= ni && !demoted) {
+                        // once a group of RD intervals: has the chain left (pll_demote) after an
+                        // interval before this one?  sdemote names it; the chain takes the barriers
+                        // of the intervals in between (those evaluations and stores are wasted and
+                        // the rest of the range is pll_demoted_kernel's, which rewrites them)
+                        if (u == 0 && !kAbNoDemote) {
+                            const int dm = __builtin_amdgcn_readfirstlane(sdemote);
+                            if (dm != 0 && dm < i) {
+                                demoted = true;
+                                return;
+                            }
+                        }
                         const unsigned long long p0 = PROF_T();
                         if (i + 1 <= ni) {
                             put(i + 1, sst[(i - 1) & 3].y, vq[sl]);  // from the phase at interval i's start
@@ -1297,7 +1360,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
                 },
                 std::make_integer_sequence<int, RD>{});
         }
-        store(ni);
+        if (!demoted) store(ni);
 #ifdef FMRX_AB_PROF
         if (t == 0 && w == 1) {
             atomicAdd(&g_idx_prof[2], ev_body);
@@ -1326,8 +1389,11 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
     if (t == 0) {
         sst[0] = make_float2(integ, phase);
         sexact[0] = 1;
+        sdemote = 0;
     }
     __syncthreads();  // (prologue)
+    uint32_t hist = 0;  // the last 32 intervals' verdicts (pll_demote)
+    int dem_i = 0;      // the interval after which the chain left (pll_demote), or 0
     unsigned long long n_redo = 0, n_inj = 0, ch_body = 0, ch_wait = 0;
     const uint32_t off = (uint32_t)(NC * ((t & (NI - 1)) % SPP));  // lane t's step's lane offset
     for (int i = 1; i <= ni; i++) {
@@ -1367,7 +1433,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         // taken (the phase), the start state in pll_batch_fast's range; test hooks force misses
         const bool lane_bad = t < NI && (uint32_t)row - off >= (uint32_t)NC;
         const bool bad = __builtin_amdgcn_ballot_w64(lane_bad) != 0 || !(phase == phase) ||
-                         !(fabsf(phase0) < kPllMaxPhase && fabsf(integ0) < kPllMaxInteg) || i == min(miss, ni) || i == inj;
+                         !(fabsf(phase0) < kPllMaxPhase && fabsf(integ0) < kPllMaxInteg) || pll_hook_miss(i, miss, ni) || i == inj;
         if (bad) {  // uniform: redo the interval exactly from its start (the chain stores it)
             n_redo++;
             n_inj += i == inj ? 1 : 0;
@@ -1381,12 +1447,28 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
             carry_exact((float)c.x, i + 1);
         }
         if (t < NI) srow[is][t] = row;
+        // demoted right after a redo (this interval's trigArgs are stored): the evaluators read
+        // sdemote at the top of their next group of intervals
+        // (bad is uniform but VGPR-derived: taken through an SGPR, so hist, the demotion and the
+        // loop exit stay scalar -- a divergent exit would turn the whole interval loop into a
+        // masked one, measured ~4 ns a step slower on the index forms)
+        const bool bad_u = __builtin_amdgcn_readfirstlane((int)bad) != 0;
+        const bool dem = !kAbNoDemote && pll_demote(hist, bad_u) && bad_u && i < ni;
         sst[is] = make_float2(integ, phase);
         sexact[is] = bad ? 1 : 0;
+        if (dem) sdemote = i;
         const unsigned long long p1 = PROF_T();
         __syncthreads();
         ch_body += p1 - p0;
         ch_wait += PROF_T() - p1;
+        if (dem) {
+            dem_i = i;
+            // the evaluators' barriers up to the top of their next group of RD intervals (from
+            // interval 1), where they read sdemote and leave
+            const int top = 1 + RD * ((i - 1) / RD + 1);
+            for (int k = i + 1; k < top && k <= ni; k++) __syncthreads();
+            break;
+        }
     }
 #ifdef FMRX_AB_PROF
     if (t == 0) {
@@ -1399,20 +1481,26 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
 #endif
     (void)ch_body;
     (void)ch_wait;
-    // the steps past the last interval exactly, from the end state
-    const long long jf = j0(ni + 1);
+    // the steps past the last interval the chain ran exactly, from the end state -- or, demoted, the
+    // exact state at jf and its step for pll_demoted_kernel (pll_demote.hip), which runs the rest
+    const long long jf = j0((dem_i ? dem_i : ni) + 1);
+    const unsigned long long n_dem = dem_i ? (unsigned long long)(n - jf) : 0ull;
     const float a = (float)(pr_at(jf - 1) + (double)phase);
     PllState q;
     PllCtx c{};
     pll_state_at(q, c, integ, phase, trig0, jf, a, DeviceLib{});
-    exact(q, c, jf, n);
+    if (n_dem == 0) exact(q, c, jf, n);
     if (t == 0) {
         S[0] = q.integ; S[1] = q.phase; S[2] = q.fbI; S[3] = q.fbQ; S[5] = q.trig;
+        S[6] = __builtin_bit_cast(float, n_dem ? (int)jf : 0);  // pll_demoted_kernel's first step, or 0
         if (stats) {
             atomicAdd(stats, n_inj);  // "resumed": the inject hook's forced redos only
             atomicAdd(stats + 1, (unsigned long long)nb);
         }
-        if (redos) atomicAdd(&redos[kPllRedoForms * (size_t)s], (unsigned)n_redo);  // form 0: index
+        if (redos) {  // fmrx_debug_pll_redos: slot 0, [2^17, 2^20)
+            atomicAdd(&redos[kPllRedoSlots * (size_t)s], (unsigned)n_redo);
+            atomicAdd(&redos[kPllRedoSlots * (size_t)s + 4], (unsigned)n_dem);
+        }
     }
 }
 
@@ -1491,6 +1579,7 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
     __shared__ int srow[4][NI];
     __shared__ float2 sst[4];
     __shared__ int sexact[4];
+    __shared__ int sdemote;  // the interval after which the chain left (pll_demote), or 0
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
     const int s = blockIdx.x;  // grid = n_streams
     const float* x = io + (size_t)s * stride;
@@ -1524,6 +1613,7 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
             exact(p, c, 0, n);
             if (t == 0) {
                 S[0] = p.integ; S[1] = p.phase; S[2] = p.fbI; S[3] = p.fbQ; S[5] = p.trig;
+                S[6] = 0.0f;  // not demoted (pll_demoted_kernel)
                 if (stats) {  // in 16-step batches, as every runner counts
                     if (!in_domain) atomicAdd(stats, (unsigned long long)(n / kPllBatch));
                     atomicAdd(stats + 1, (unsigned long long)(n / kPllBatch));
@@ -1597,13 +1687,27 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
         ld(1 + RD, vq[1 % RD]);
         __syncthreads();  // (prologue)
         unsigned long long ev_body = 0, ev_wait = 0;
-        for (int i0 = 1; i0 <= ni; i0 += RD) {
+        // the chain demoted the stream (pll_demote) after redoing interval i - 1 itself: it runs the
+        // rest of the range alone, no barrier is reached any more
+        bool demoted = false;
+        for (int i0 = 1; i0 <= ni && !demoted; i0 += RD) {
             unroll_ic(
                 [&](auto uc) {
                     constexpr int u = decltype(uc)::value;
                     constexpr int sl = (2 + u) % RD;  // slot of interval i + 1
                     const int i = i0 + u;
-                    if (i <= ni) {
+                    if (i <= ni && !demoted) {
+                        // once a group of RD intervals: has the chain left (pll_demote) after an
+                        // interval before this one?  sdemote names it; the chain takes the barriers
+                        // of the intervals in between (those evaluations and stores are wasted and
+                        // the rest of the range is pll_demoted_kernel's, which rewrites them)
+                        if (u == 0 && !kAbNoDemote) {
+                            const int dm = __builtin_amdgcn_readfirstlane(sdemote);
+                            if (dm != 0 && dm < i) {
+                                demoted = true;
+                                return;
+                            }
+                        }
                         const unsigned long long p0 = PROF_T();
                         if (i + 1 <= ni) {
                             put(i + 1, sst[(i - 1) & 3].y, vq[sl]);  // from the phase at interval i's start
@@ -1618,7 +1722,7 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
                 },
                 std::make_integer_sequence<int, RD>{});
         }
-        store(ni);
+        if (!demoted) store(ni);
 #ifdef FMRX_AB_PROF
         if (t == 0 && w == 1) {
             atomicAdd(&g_cnt_prof[2], ev_body);
@@ -1647,8 +1751,11 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
     if (t == 0) {
         sst[0] = make_float2(integ, phase);
         sexact[0] = 1;
+        sdemote = 0;
     }
     __syncthreads();  // (prologue)
+    uint32_t hist = 0;  // the last 32 intervals' verdicts (pll_demote)
+    int dem_i = 0;      // the interval after which the chain left (pll_demote), or 0
     unsigned long long n_redo = 0, n_inj = 0, ch_body = 0, ch_wait = 0;
     const int ls = t < NP ? t : NP - 1;  // this lane's row slot (lanes past the row read its last)
     for (int i = 1; i <= ni; i++) {
@@ -1693,7 +1800,7 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
         // start state in pll_batch_fast's range; test hooks force misses
         const float ce = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cE), cC));
         const bool bad = !(phase == phase) || !(ce == ce) ||
-                         !(fabsf(phase0) < kPllMaxPhase && fabsf(integ0) < kPllMaxInteg) || i == min(miss, ni) ||
+                         !(fabsf(phase0) < kPllMaxPhase && fabsf(integ0) < kPllMaxInteg) || pll_hook_miss(i, miss, ni) ||
                          i == inj;
         if (bad) {  // uniform: redo the interval exactly from its start (the chain stores it)
             n_redo++;
@@ -1710,12 +1817,27 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
 #pragma unroll
         for (int r = 0; r < NRW; r++)
             if (t + 64 * r < NI) srow[is][t + 64 * r] = row[r];
+        // demoted right after a redo (pll_idx_kernel's rule)
+        // (bad is uniform but VGPR-derived: taken through an SGPR, so hist, the demotion and the
+        // loop exit stay scalar -- a divergent exit would turn the whole interval loop into a
+        // masked one, measured ~4 ns a step slower on the index forms)
+        const bool bad_u = __builtin_amdgcn_readfirstlane((int)bad) != 0;
+        const bool dem = !kAbNoDemote && pll_demote(hist, bad_u) && bad_u && i < ni;
         sst[is] = make_float2(integ, phase);
         sexact[is] = bad ? 1 : 0;
+        if (dem) sdemote = i;
         const unsigned long long p1 = PROF_T();
         __syncthreads();
         ch_body += p1 - p0;
         ch_wait += PROF_T() - p1;
+        if (dem) {
+            dem_i = i;
+            // the evaluators' barriers up to the top of their next group of RD intervals (from
+            // interval 1), where they read sdemote and leave
+            const int top = 1 + RD * ((i - 1) / RD + 1);
+            for (int k = i + 1; k < top && k <= ni; k++) __syncthreads();
+            break;
+        }
     }
 #ifdef FMRX_AB_PROF
     if (t == 0) {
@@ -1727,21 +1849,26 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
 #endif
     (void)ch_body;
     (void)ch_wait;
-    // the steps past the last interval exactly, from the end state
-    const long long jf = j0(ni + 1);
+    // the steps past the last interval the chain ran exactly, from the end state -- or, demoted, the
+    // exact state at jf and its step for pll_demoted_kernel (pll_demote.hip), which runs the rest
+    const long long jf = j0((dem_i ? dem_i : ni) + 1);
+    const unsigned long long n_dem = dem_i ? (unsigned long long)(n - jf) : 0ull;
     const float a = (float)(pr_at(jf - 1) + (double)phase);
     PllState q;
     PllCtx c{};
     pll_state_at(q, c, integ, phase, trig0, jf, a, DeviceLib{});
-    exact(q, c, jf, n);
+    if (n_dem == 0) exact(q, c, jf, n);
     if (t == 0) {
         S[0] = q.integ; S[1] = q.phase; S[2] = q.fbI; S[3] = q.fbQ; S[5] = q.trig;
+        S[6] = __builtin_bit_cast(float, n_dem ? (int)jf : 0);  // pll_demoted_kernel's first step, or 0
         if (stats) {  // in 16-step batches, as every runner counts
             atomicAdd(stats, n_inj * (NI / kPllBatch));  // "resumed": the inject hook's forced redos only
             atomicAdd(stats + 1, (unsigned long long)(n / kPllBatch));
         }
-        if (redos) atomicAdd(&redos[kPllRedoForms * (size_t)s + (lo < kPllPipeMinLow ? 0 : lo < kPllPipeMin5 ? 1 : lo < kPllPipeMin ? 2 : 3)],
-                             (unsigned)n_redo);
+        if (redos) {  // fmrx_debug_pll_redos, by the range's trigOffset
+            atomicAdd(&redos[kPllRedoSlots * (size_t)s + pll_redo_range(lo)], (unsigned)n_redo);
+            atomicAdd(&redos[kPllRedoSlots * (size_t)s + 4 + pll_redo_range(lo)], (unsigned)n_dem);
+        }
     }
 }
 

@@ -1080,6 +1080,9 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
             else
                 launch_pll_pipe(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j, (size_t)n,
                                 inject, pipe_miss, form, spec_stats, hint.redos);
+            // the streams that launch demoted (an unlocked loop): the rest of its range
+            idx_rc |= launch_pll_demoted(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j,
+                                         (size_t)n, inject, spec_stats);
         });
         j = e;
     }

@@ -11,6 +11,11 @@
 //            a_k (75k / f_k) * {-cos | sin}(2 pi f_k t)
 //   I,Q = cos(phi), sin(phi);  u8 = clamp(128 + round(100 x) + noise), noise ~ N(0, 2 LSB)
 //   (sigma 0.02 of full scale), from a counter-based hash of (seed, n).
+//
+// Variants for the PLL's unlocked regimes, selected by the seed's top byte (seeds below 2^56 are
+// the plain signal; the tones follow the low 56 bits): kSynthNoPilot drops the 19 kHz pilot (a
+// mono broadcast: the reference PLL, filter.cpp:157-171, then never locks), and noise shift k
+// (bits 57-59) scales the noise by 2^k (k = 3: sigma ~16 LSB against a carrier of 100).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -20,9 +25,12 @@ namespace fmrx {
 constexpr int kSynthTones = 7;
 constexpr int kSinBits = 14;  // 16384-entry Q15 sine table
 constexpr int kSinSize = 1 << kSinBits;
+constexpr uint64_t kSynthNoPilot = 1ull << 56;
+constexpr int kSynthNoiseShiftBit = 57;  // 3 bits
 
 struct SynthParams {
     uint64_t seed;
+    int noise_shift;              // noise x 2^noise_shift (seed bits 57-59)
     int64_t amp[kSynthTones];     // phase amplitude in 2^-32-turn units, Q15-scaled table
     uint64_t inc[kSynthTones];    // phase increment per sample, 2^-32 turn units (64-bit)
     uint32_t off[kSynthTones];    // phase offset (0 for sin, -pi/2 for -cos)
@@ -62,8 +70,8 @@ __host__ __device__ inline void synth_pair(const SynthParams& p, const int16_t* 
     const int c = sintab[(uint32_t)(phi + 0x40000000u) >> (32 - kSinBits)];  // cos = sin(+pi/2)
     const int s = sintab[phi >> (32 - kSinBits)];
     const uint64_t h = splitmix64(p.seed * 0xD1B54A32D192ED03ull ^ n);
-    iq[0] = synth_quant(c, synth_noise((uint32_t)h));
-    iq[1] = synth_quant(s, synth_noise((uint32_t)(h >> 32)));
+    iq[0] = synth_quant(c, synth_noise((uint32_t)h) * (1 << p.noise_shift));
+    iq[1] = synth_quant(s, synth_noise((uint32_t)(h >> 32)) * (1 << p.noise_shift));
 }
 
 // Host-side parameter setup (double math, done once per stream).

@@ -142,7 +142,8 @@ def gather_chunked(chunks, n_streams: int, pcm_len: int, world: int, rank: int, 
 
 def run_leg(setup: Callable[[], object], process: Callable[[object], torch.Tensor], n_streams: int, pcm_len: int,
             world: int, rank: int, pg: bool, device=None, cleanup: Callable[[object], None] | None = None,
-            post: Callable[[object], dict] | None = None) -> dict:
+            post: Callable[[object], dict] | None = None, repeats: int = 1,
+            reset: Callable[[object], None] | None = None) -> dict:
     """One timed multi-stream step with failure agreement (the collective skeleton of
     streams_leg, also run on the CPU with gloo by the tests).
 
@@ -151,7 +152,9 @@ def run_leg(setup: Callable[[], object], process: Callable[[object], torch.Tenso
     the barrier and again before the gather every rank agrees on success (all_ok), so a rank
     that raised does not leave the others in a collective.  Returns a dict on every rank:
     `error` when any rank failed, else per-rank seconds (total, process, gather) and, on rank 0,
-    `gathered` ([n_streams, pcm_len])."""
+    `gathered` ([n_streams, pcm_len]).  repeats > 1: the timed step that many times, reset(state)
+    (untimed) before each after the first; the result is the repeat of median total time, with
+    `runs` (every repeat's max-over-ranks total) beside it, and the last repeat's PCM."""
     import time
 
     err, state = None, None
@@ -162,32 +165,44 @@ def run_leg(setup: Callable[[], object], process: Callable[[object], torch.Tenso
     try:
         if not all_ok(err is None, pg, device):
             return {"error": err or "another rank failed in setup; collectives skipped"}
-        if pg:
-            dist.barrier()
-        if device is not None and torch.cuda.is_available():
-            torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        local = None
-        try:
-            local = process(state)
+        reps = []
+        for rep in range(max(1, repeats)):
+            if rep > 0 and reset is not None:
+                try:
+                    reset(state)
+                except Exception as e:  # noqa: BLE001
+                    err = f"rank {rank} reset: {e!r}"
+                if not all_ok(err is None, pg, device):
+                    return {"error": err or "another rank failed in a reset; collectives skipped"}
+            if pg:
+                dist.barrier()
+            if device is not None and torch.cuda.is_available():
+                torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            local = None
+            try:
+                local = process(state)
+                if isinstance(local, torch.Tensor):
+                    assert local.shape[1:] == (pcm_len,), (tuple(local.shape), pcm_len)
+            except Exception as e:  # noqa: BLE001
+                err = f"rank {rank} process: {e!r}"
+            t1 = time.perf_counter()
+            if not all_ok(err is None, pg, device):
+                return {"error": err or "another rank failed in the timed step; gather skipped"}
             if isinstance(local, torch.Tensor):
-                assert local.shape[1:] == (pcm_len,), (tuple(local.shape), pcm_len)
-        except Exception as e:  # noqa: BLE001
-            err = f"rank {rank} process: {e!r}"
-        t1 = time.perf_counter()
-        if not all_ok(err is None, pg, device):
-            return {"error": err or "another rank failed in the timed step; gather skipped"}
-        if isinstance(local, torch.Tensor):
-            gathered = gather_pcm(local, n_streams, pcm_len, world, rank) if pg else local
-            t_proc = t1
-        else:  # time chunks enqueued: each gathered as soon as it is done, beside the later ones
-            gathered, t_proc = gather_chunked(local, n_streams, pcm_len, world, rank, pg)
-        if device is not None and torch.cuda.is_available():
-            torch.cuda.synchronize(device)
-        t2 = time.perf_counter()
-        ranks = per_rank([t2 - t0, t_proc - t0, t2 - t_proc], pg, device)
-        res = {"per_rank": ranks, "total": max(r[0] for r in ranks), "process": max(r[1] for r in ranks),
-               "gather": max(r[2] for r in ranks)}
+                gathered = gather_pcm(local, n_streams, pcm_len, world, rank) if pg else local
+                t_proc = t1
+            else:  # time chunks enqueued: each gathered as soon as it is done, beside the later ones
+                gathered, t_proc = gather_chunked(local, n_streams, pcm_len, world, rank, pg)
+            if device is not None and torch.cuda.is_available():
+                torch.cuda.synchronize(device)
+            t2 = time.perf_counter()
+            ranks = per_rank([t2 - t0, t_proc - t0, t2 - t_proc], pg, device)
+            reps.append({"per_rank": ranks, "total": max(r[0] for r in ranks), "process": max(r[1] for r in ranks),
+                         "gather": max(r[2] for r in ranks)})
+        order = sorted(range(len(reps)), key=lambda k: reps[k]["total"])
+        res = dict(reps[order[len(order) // 2]])
+        res["runs"] = [r["total"] for r in reps]
         if rank == 0:
             res["gathered"] = gathered
             if post is not None:  # after the timed step, untimed (rank 0's shard only)
@@ -204,7 +219,7 @@ def run_leg(setup: Callable[[], object], process: Callable[[object], torch.Tenso
 def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, device: int,
                 mode: int = 0, expect: dict | None = None, warmup: bool = True,
                 collective: bool | None = None, profile: Callable | None = None,
-                gather_chunks: int = 1) -> dict | None:
+                gather_chunks: int = 1, repeats: int = 1) -> dict | None:
     """BASELINE configs[4] as one timed step: `n_streams` independent stereo streams (stream id
     = synth seed) of `seconds` each, this rank's contiguous shard processed as ONE multi-stream
     device-resident call, then the S16 PCM gathered to rank 0 (RCCL over xGMI; gloo rehearses
@@ -221,7 +236,10 @@ def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, dev
     `gather_chunks` K > 1 (with a process group): the shard runs as K calls over consecutive time
     chunks (the context carries every state across them: the same PCM as one call), each chunk's
     PCM gathered as soon as it is done while the next is processed (gather_chunked), so only the
-    last chunk's gather follows the processing.  Returns rank 0's result dict (None elsewhere)."""
+    last chunk's gather follows the processing.  `repeats`: the timed step that many times from
+    the power-on state (fmrx_reset between them, untimed): the line's times are the median
+    repeat's, `runs` / `median` / `min` / `max` the totals.  Returns rank 0's result dict (None
+    elsewhere)."""
     import hashlib
     import time
 
@@ -235,7 +253,7 @@ def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, dev
     K = max(1, min(gather_chunks, nb)) if pg else 1
     cuts = [nb * k // K for k in range(K + 1)]  # block boundaries of the time chunks
     t_synth = [0.0]
-    redos = [None]  # this rank's streams x 4 redone intervals (fmrx_debug_pll_redos), warm-up call
+    redos = [None]  # this rank's streams x 8 redo slots (fmrx_debug_pll_redos), warm-up call
 
     def setup():
         rx = fmrx.Receiver(mode, fmrx.STEREO, n_streams=max(1, len(ids)), device=device)
@@ -256,7 +274,7 @@ def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, dev
             if ids and warmup:
                 # the untimed warm-up does the timed step's work exactly (same input, same
                 # power-on state): the runners' per-stream redo counts are taken here
-                redo = torch.zeros((len(ids), 4), dtype=torch.int32, device=dev)
+                redo = torch.zeros((len(ids), fmrx.REDO_SLOTS), dtype=torch.int32, device=dev)
                 rx.debug_pll_redos(redo.data_ptr())
                 for k in range(K):
                     rx.process_device(iqs[k].data_ptr(), cuts[k + 1] - cuts[k], outs[k].data_ptr())
@@ -296,8 +314,12 @@ def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, dev
                 for k in range(K):
                     st[0].process_device(st[1][k].data_ptr(), cuts[k + 1] - cuts[k], st[2][k].data_ptr())
             return profile(st[0], run)
+    def reset(st):
+        st[0].reset()
+        st[0].synchronize()
+
     res = run_leg(setup, process, n_streams, pcm_len, world, rank, pg, dev, cleanup=lambda st: st[0].close(),
-                  post=post)
+                  post=post, repeats=repeats, reset=reset)
     if rank != 0:
         return None
     if "error" in res:
@@ -313,6 +335,12 @@ def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, dev
                        + (f" in {K} time chunks, each gathered beside the next one's processing" if K > 1 else ""),
            "n_gpus": world, "seconds": round(total, 4), "seconds_process": round(res["process"], 4),
            "seconds_gather": round(res["gather"], 4), "gather_bytes": int(gathered.numel() * 2),
+           "seconds_note": ("seconds_process ends when the last time chunk's processing is seen complete and "
+                            "includes the gathers of the chunks before it (overlapped with processing on RCCL, "
+                            "host-blocking on gloo); seconds_gather is the last chunk's gather only")
+           if K > 1 else "seconds_process: the call; seconds_gather: the gather after it",
+           "runs": [round(x, 4) for x in res["runs"]], "median": round(total, 4),
+           "min": round(min(res["runs"]), 4), "max": round(max(res["runs"]), 4),
            "gather_chunks": K,
            # every rank sends an equal (padded) message per chunk; rank 0 receives world of them
            "gather_bytes_sent_per_rank": int(max_local * pcm_len * 2) if pg else 0,
@@ -331,14 +359,18 @@ def streams_leg(fmrx, n_streams: int, seconds: float, world: int, rank: int, dev
     if redos[0] is not None and len(ids):
         # rank 0's shard: the streams whose redone intervals (a trigArg outside the runner's
         # candidates) cost the most serial time -- the slowest of them sets the call's wall time
-        r = redos[0]
+        r, dm = redos[0][:, :4], redos[0][:, 4:]
         tot = r.sum(axis=1)
         worst = [int(i) for i in tot.argsort()[::-1][:8]]
-        out["redos"] = {"streams": len(ids), "forms": ["index", "pipe16", "pipe64_five", "pipe_three"],
-                        "total_per_form": [int(x) for x in r.sum(axis=0)],
-                        "max_per_form": [int(x) for x in r.max(axis=0)],
+        out["redos"] = {"streams": len(ids), "ranges": fmrx.REDO_RANGES,
+                        "total_per_range": [int(x) for x in r.sum(axis=0)],
+                        "max_per_range": [int(x) for x in r.max(axis=0)],
                         "worst_streams": [{"stream": ids[i], "redos": [int(x) for x in r[i]]} for i in worst],
-                        "source": "fmrx_debug_pll_redos over the untimed warm-up call (same input, same state)"}
+                        "demoted_streams": int((dm.sum(axis=1) > 0).sum()),
+                        "demoted_steps_per_range": [int(x) for x in dm.sum(axis=0)],
+                        "source": "fmrx_debug_pll_redos over the untimed warm-up call (same input, same state): "
+                                  "redone intervals by the runner launch's trigOffset range; demoted: steps run on "
+                                  "the exact path after most intervals missed (pll_demote)"}
     if expect:
         host = gathered.cpu().numpy()
         got = {sid: hashlib.sha256(host[sid].tobytes()).hexdigest() for sid in expect}

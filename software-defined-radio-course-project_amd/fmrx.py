@@ -104,6 +104,9 @@ KNOBS = {"pll_spec": 0, "pll_sat": 1, "pll_pred": 2, "pll_pipe": 3, "pll_idx": 4
          "mono_split": 6, "bpf_tile": 7, "halo_kernel": 8, "pll_inject": 9, "pll_pipe_miss": 10,
          "pll_hint_skew": 11, "pll_cnt": 12, "pll_stick": 13, "stereo_head": 14,
          "stereo_lead": 15, "audio_defer": 16, "stereo_tail": 17}
+# fmrx_debug_pll_redos's trigOffset ranges (slots r and 4 + r of each stream's 8)
+REDO_RANGES = ["[2^17,2^20)", "[2^20,2^21)", "[2^21,2^22)", "[2^22,2^24]"]
+REDO_SLOTS = 8
 # knobs every new Receiver applies after fmrx_create (tests set it per test, e.g. with
 # monkeypatch.setattr; the library itself reads only the tuning knobs' environment variables)
 DEFAULT_KNOBS: dict = {}
@@ -401,8 +404,9 @@ class Receiver:
         _check(lib().fmrx_debug_pll_stats(self.h, d_counts))
 
     def debug_pll_redos(self, d_counts) -> None:
-        """fmrx_debug_pll_redos: per-stream redone intervals of the self-certifying runners
-        (n_streams x 4 u32 on the device, zeroed by the caller; None turns it off)."""
+        """fmrx_debug_pll_redos: per stream and trigOffset range of the self-certifying runners
+        (REDO_RANGES), redone intervals and demoted steps (n_streams x 8 u32 on the device, zeroed
+        by the caller: [r] redone intervals, [4 + r] demoted steps; None turns it off)."""
         _check(lib().fmrx_debug_pll_redos(self.h, d_counts))
 
 

@@ -89,7 +89,13 @@ def _hashes():
 
 def long_runs():
     """Long-run hashes (2-100 s of signal): pcm, pcm_mono and the last PLL state."""
-    return {k: v for k, v in _hashes().items() if not k.startswith(("bench_", "streams_"))}
+    return {k: v for k, v in _hashes().items() if not k.startswith(("bench_", "streams_", "unlocked_"))}
+
+
+def unlocked_runs():
+    """Long-run hashes of streams whose PLL never locks or slips (72-80 s, past the trigOffset
+    stick): random bytes, no pilot, heavy noise, mode 2's PLL at the upsampled if_fs."""
+    return {k: v for k, v in _hashes().items() if k.startswith("unlocked_")}
 
 
 def stream_runs():

@@ -75,13 +75,30 @@ def leg_chunked(d, n_streams, world, rank, n_chunks=3):
     return d.run_leg(lambda: list(d.shard(n_streams, world, rank)), run, n_streams, NB * NA * 2, world, rank, True)
 
 
+def leg_repeats(d, n_streams, world, rank, repeats=3):
+    """dist.run_leg timing the step `repeats` times with a reset between (bench.py's configs[4]
+    median of repeats): every repeat gathers; the result carries every repeat's total."""
+    resets = []
+
+    def reset(ids):
+        resets.append(len(ids))
+
+    res = d.run_leg(lambda: list(d.shard(n_streams, world, rank)), process, n_streams, NB * NA * 2, world, rank,
+                    True, repeats=repeats, reset=reset)
+    assert len(resets) == repeats - 1, resets
+    if rank == 0:
+        assert len(res["runs"]) == repeats and res["total"] == sorted(res["runs"])[repeats // 2], res
+    return res
+
+
 def main():
     n_streams, out_path = int(sys.argv[1]), sys.argv[2]
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     d = iqgen.load_module("dist")
-    if len(sys.argv) > 3 and sys.argv[3] in ("setup", "process", "ok", "chunks"):  # dist.run_leg
+    if len(sys.argv) > 3 and sys.argv[3] in ("setup", "process", "ok", "chunks", "repeats"):  # dist.run_leg
         res = (leg_chunked(d, n_streams, world, rank) if sys.argv[3] == "chunks"
+               else leg_repeats(d, n_streams, world, rank) if sys.argv[3] == "repeats"
                else leg_with_failure(d, n_streams, world, rank, sys.argv[3]))
         if rank == 0:
             if "error" in res:

@@ -3,6 +3,10 @@
 Recipes:
   ``synth:<seed>``  FM-stereo synthetic signal from libfmrx's integer-only generator
                     (fmrx_synth_host; identical bytes to the GPU generator)
+  ``nopilot:<seed>`` the same generator without the 19 kHz pilot (a mono broadcast: the
+                    reference PLL never locks); seed | 2^56 (csrc/synth.h kSynthNoPilot)
+  ``noisy:<seed>``  the same generator with 64x the noise (sigma ~128 LSB, clipped): the loop
+                    slips cycles; seed | 6 << 57
   ``rand:<seed>``   uniform random bytes, splitmix64 counter hash in numpy (version-proof)
   ``const<v>``      every byte = v (``const128`` is x = 0.0)
 """
@@ -59,14 +63,22 @@ def splitmix64(x: np.ndarray) -> np.ndarray:
 
 
 def rand_bytes(seed: int, n: int) -> np.ndarray:
-    idx = np.arange(n, dtype=np.uint64) + (np.uint64(seed) << np.uint64(40))
-    return (splitmix64(idx) >> np.uint64(29)).astype(np.uint8)
+    out = np.empty(n, np.uint8)
+    step = 1 << 24  # chunked: a 72 s stream is 345.6 MB
+    for a in range(0, n, step):
+        idx = np.arange(a, min(n, a + step), dtype=np.uint64) + (np.uint64(seed) << np.uint64(40))
+        out[a: a + idx.size] = (splitmix64(idx) >> np.uint64(29)).astype(np.uint8)
+    return out
+
+
+SYNTH_FLAGS = {"synth": 0, "nopilot": 1 << 56, "noisy": 6 << 57}
 
 
 def make(recipe: str, n_bytes: int, rf_fs: int = 2400000) -> np.ndarray:
-    if recipe.startswith("synth:"):
+    kind, _, arg = recipe.partition(":")
+    if kind in SYNTH_FLAGS:
         fm = load_fmrx()
-        return fm.synth_host(int(recipe[6:]), rf_fs, 0, n_bytes // 2)
+        return fm.synth_host(int(arg) | SYNTH_FLAGS[kind], rf_fs, 0, n_bytes // 2)
     if recipe.startswith("rand:"):
         return rand_bytes(int(recipe[5:]), n_bytes)
     if recipe.startswith("const"):

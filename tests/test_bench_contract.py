@@ -35,6 +35,11 @@ def test_bench_json_contract():
     oc = j["baseline_configs"]  # the other single-GPU BASELINE configs, same box
     assert "error" not in oc, oc
     assert oc["configs[2]"]["x_realtime"] > 1 and oc["configs[3]"]["MS_per_s"] > 0
+    # configs[2] and configs[4] timed five times each (bench.py --repeats): median, min, max
+    for c in ("configs[2]", "configs[4]"):
+        r = oc[c]
+        assert len(r["runs"]) == 5 and r["min"] <= r["median"] <= r["max"], r
+    assert oc["configs[2]"]["seconds"] == round(oc["configs[2]"]["median"], 3)
     # full-size parity of both extra configs against the reference build's PCM hashes of the
     # same bytes (tests/golden/hashes.json bench_*): /root/reference/src/project.cpp:132-196
     for c in ("configs[2]", "configs[3]"):

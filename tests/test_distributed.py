@@ -88,3 +88,11 @@ def test_run_leg_world2_gathers_time_chunks(orc, tmp_path):
     got = _run_world2(tmp_path, 3, "chunks")
     want = np.stack([orc.run(MODE, 51, iqgen.make(f"rand:{100 + i}", NB * BB), ["pcm"])["pcm"] for i in range(3)])
     assert np.array_equal(got, want)
+
+
+def test_run_leg_world2_repeats(orc, tmp_path):
+    """The timed step repeated (bench.py's configs[4] median of five): reset between repeats, every
+    repeat gathers, the median repeat's times reported beside all of them; the same PCM."""
+    got = _run_world2(tmp_path, 3, "repeats")
+    want = np.stack([orc.run(MODE, 51, iqgen.make(f"rand:{100 + i}", NB * BB), ["pcm"])["pcm"] for i in range(3)])
+    assert np.array_equal(got, want)

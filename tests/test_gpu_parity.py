@@ -16,7 +16,7 @@ import pytest
 
 import iqgen
 import oracle
-from conftest import bench_runs, case_input, golden_cases, load_case, long_runs
+from conftest import bench_runs, case_input, golden_cases, load_case, long_runs, unlocked_runs
 
 pytestmark = pytest.mark.gpu
 
@@ -692,6 +692,51 @@ def test_saturated_runner_wide_grid(fmrx):
             assert np.array_equal(r1.process(ins[s, 2 * bb:]), out[s]), s
 
 
+def _unlocked_input(rx, h):
+    """A fixture's input on the device: the synth recipes generated there (identical bytes),
+    random bytes uploaded."""
+    n = h["n_blocks"] * rx.geo.block_bytes
+    d = torch.empty(n, dtype=torch.uint8, device="cuda")
+    kind, _, arg = h["recipe"].partition(":")
+    if kind in iqgen.SYNTH_FLAGS:
+        rx.synth_device(int(arg) | iqgen.SYNTH_FLAGS[kind], 0, n // 2, d.data_ptr())
+        rx.synchronize()
+    else:
+        d.copy_(torch.from_numpy(iqgen.make(h["recipe"], n, rx.geo.rf_fs)))
+    assert sha(d.cpu().numpy()) == h["input_sha256"]
+    return d
+
+
+def _pll_floats(rx):
+    """A 1-stream context's PLL state {integrator, phaseEst, fbI, fbQ, ncoOut_state, trigOffset}
+    from its state blob (api.cpp state_io order: halo, audio history, demod history, PLL)."""
+    blob = rx.get_state()
+    hdr = np.frombuffer(blob[:40], np.uint32)
+    off = 40 + int(hdr[6]) + 4 * int(hdr[7]) + 4 * 64
+    return np.frombuffer(blob[off: off + 24], np.float32)
+
+
+@pytest.mark.parametrize("name", sorted(unlocked_runs()))
+def test_unlocked_pll_long_hash(fmrx, name):
+    """The PLL where it never locks or slips cycles (filter.cpp:157-171; random bytes, no pilot,
+    heavy noise, mode 2's PLL handed the upsampled if_fs, project.cpp:166,348), 17-19 M steps
+    each, through every runner form and the trigOffset stick: one device-resident call, the PCM
+    and the final PLL state against the reference build's."""
+    h = unlocked_runs()[name]
+    with fmrx.Receiver(h["mode"], fmrx.STEREO, rf_taps=h["rf_taps"]) as rx:
+        d_iq = _unlocked_input(rx, h)
+        d_pcm = torch.empty(h["n_blocks"] * rx.geo.pcm_samples, dtype=torch.int16, device="cuda")
+        redos = torch.zeros(fmrx.REDO_SLOTS, dtype=torch.int32, device="cuda")
+        rx.debug_pll_redos(redos.data_ptr())
+        rx.process_device(d_iq.data_ptr(), h["n_blocks"], d_pcm.data_ptr())
+        rx.synchronize()
+        rx.debug_pll_redos(None)
+        assert sha(d_pcm.cpu().numpy()) == h["pcm_sha256"], name
+        assert same(_pll_floats(rx), np.asarray(h["pll_state_last"], np.float32))
+    # every one of these streams misses most intervals somewhere: demoted there
+    assert redos.cpu().numpy()[4:].sum() > 0, redos.cpu().numpy()
+
+
 @pytest.mark.parametrize("name", [n for n in long_runs() if long_runs()[n]["mode"] in (2, 3)])
 def test_polyphase_mono_long_hash(fmrx, name):
     h = long_runs()[name]
@@ -1061,7 +1106,7 @@ def test_count_runner_streams(fmrx, monkeypatch):
             blob[pll_off: pll_off + ns * 32] = pll.tobytes()
             rx.set_state(bytes(blob))
             counts = torch.zeros(2, dtype=torch.int64, device="cuda")
-            redos = torch.zeros((ns, 4), dtype=torch.int32, device="cuda")
+            redos = torch.zeros((ns, fmrx.REDO_SLOTS), dtype=torch.int32, device="cuda")
             rx.debug_pll_stats(counts.data_ptr())
             rx.debug_pll_redos(redos.data_ptr())
             outs.append(rx.process(ins[:, 2 * bb:]))
@@ -1069,8 +1114,94 @@ def test_count_runner_streams(fmrx, monkeypatch):
             rx.debug_pll_redos(None)
         resumed, checked = counts.cpu().tolist()
         assert checked > 0 and resumed == 0, (cnt, resumed, checked)
-        assert int(redos.sum()) >= 0
+        r = redos.cpu().numpy()
+        # locked streams: no demotion, and nothing below 2^19 or past 2^21 in this range
+        assert not r[:, 4:].any() and not r[:, 2:4].any(), r.sum(axis=0)
     assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("trig0,slots", [(4194304.0 - 6000.0, (2, 3)), (1048576.0 - 3000.0, (0, 1)),
+                                         (300000.0, (0,))])
+def test_pll_redo_slots(fmrx, monkeypatch, trig0, slots):
+    """fmrx_debug_pll_redos files each runner launch's redone intervals by its trigOffset range
+    (fmrx.REDO_RANGES): 4 streams put at trig0 through the state blob run 24 blocks (15,360 steps)
+    with knob pll_pipe_miss = 3 (interval 3 of every launch reported missed) and without.  Hooked:
+    every stream has at least one redo in each range the call crosses (`slots`); every slot of a
+    range it does not cross is zero, hooked or not (redos and demoted steps); the PCM is
+    identical."""
+    ns, nb, bb = 4, 24, 12800
+    ins = np.stack([iqgen.make("synth:%d" % (760 + s), (nb + 2) * bb) for s in range(ns)])
+    res = {}
+    for hook in (None, 3):
+        knobs(monkeypatch, fmrx, pll_pipe_miss=-1 if hook is None else hook)
+        with fmrx.Receiver(0, fmrx.STEREO, n_streams=ns) as rx:
+            rx.process(ins[:, : 2 * bb])
+            blob = bytearray(rx.get_state())
+            hdr = np.frombuffer(bytes(blob[:40]), np.uint32)
+            pll_off = 40 + ns * (int(hdr[6]) + 4 * int(hdr[7]) + 4 * 64)
+            pll = np.frombuffer(bytes(blob[pll_off: pll_off + ns * 32]), np.float32).reshape(ns, 8).copy()
+            pll[:, 5] = trig0
+            blob[pll_off: pll_off + ns * 32] = pll.tobytes()
+            rx.set_state(bytes(blob))
+            redos = torch.zeros((ns, fmrx.REDO_SLOTS), dtype=torch.int32, device="cuda")
+            rx.debug_pll_redos(redos.data_ptr())
+            out = rx.process(ins[:, 2 * bb:])
+            rx.debug_pll_redos(None)
+        res[hook] = (out, redos.cpu().numpy())
+    (o0, r0), (o1, r1) = res[None], res[3]
+    assert np.array_equal(o0, o1)
+    # (the PLL state put out of its loop's lock makes some streams miss most intervals for a while:
+    # those demote, with their demoted steps in the same range's slot)
+    for sl in range(4):
+        if sl in slots:
+            assert (r1[:, sl] >= 1).all(), (sl, r0[:, sl], r1[:, sl])
+        else:
+            for r in (r0, r1):
+                assert not r[:, sl].any() and not r[:, 4 + sl].any(), (sl, r0, r1)
+
+
+@pytest.mark.parametrize("trig0", [131100.0, 300000.0, 700000.0, 1500000.0, 3000000.0, 6000000.0, 16770000.0,
+                                   16777216.0])
+@pytest.mark.parametrize("miss", [-2, -40])
+@pytest.mark.parametrize("cnt", [12, 0])
+@pytest.mark.parametrize("inject", [None, 3])
+def test_pll_demotion(fmrx, orc, monkeypatch, trig0, miss, cnt, inject):
+    """A stream whose intervals keep missing (an unlocked loop; forced here by knob pll_pipe_miss
+    = -k: every interval from k - 1 on) is demoted by each self-certifying runner once 24 of its
+    last 32 intervals missed: the rest of the launch's range runs on the exact path
+    (pll_run_fast).  20,000 steps from each form's range (index 2^17 / 2^18, count or index 2^19,
+    count or 16-step three-wave 2^20, five-candidate 2^21, three-candidate 2^22, the stick's
+    handover and the stick): bit-exact against the oracle, state included, and the demoted steps
+    filed in the range's slot.  pll_inject: the runners and the demoted stream's chain (pll_demote.hip)
+    each corrupt one batch -- the checkers catch it, the chain recomputes from there (resumed)."""
+    knobs(monkeypatch, fmrx, pll_pipe_miss=miss, pll_cnt=cnt)
+    if inject is not None:
+        knobs(monkeypatch, fmrx, pll_inject=inject)
+    n = 20000
+    rng = np.random.default_rng(int(trig0) % 997)
+    t = np.arange(n)
+    x = (0.1 * np.cos(2 * np.pi * 19000 / 240000 * t + 0.3) + 0.02 * rng.standard_normal(n)).astype(np.float32)
+    st0 = np.array([1e-4, 0.4, 0.6, 0.8, 1.0, trig0], np.float32)
+    want_x, want_st = orc.pll(x, 19000, 240000, 2.0, 0.0, 0.01, st0)
+    with fmrx.Receiver(0, fmrx.STEREO) as rx:
+        buf = _d(x)
+        st = _d(st0)
+        redos = torch.zeros(fmrx.REDO_SLOTS, dtype=torch.int32, device="cuda")
+        counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+        rx.debug_pll_redos(redos.data_ptr())
+        rx.debug_pll_stats(counts.data_ptr())
+        torch.cuda.synchronize()
+        rx.pll(buf.data_ptr(), n, 19000, 240000, 2.0, 0.0, 0.01, st.data_ptr())
+        rx.synchronize()
+        rx.debug_pll_redos(None)
+        rx.debug_pll_stats(None)
+        assert same(buf.cpu().numpy(), want_x)
+        assert same(st.cpu().numpy(), want_st)
+    r = redos.cpu().numpy()
+    if miss == -2:  # (from interval 39 on, a short launch may end before 24 misses)
+        assert r[4:].sum() > 0, r
+        if inject is not None:
+            assert counts.cpu().tolist()[0] > 0
 
 
 @pytest.mark.parametrize("mixed", [False, True])
@@ -1172,7 +1303,7 @@ def test_device_synth_equals_host(fmrx):
         rx.synchronize()
         assert np.array_equal(d.cpu().numpy(), fmrx.synth_host(9, 2400000, 123456, 300001))
         # several streams in one launch (configs[4]'s per-rank input), rows with a gap between
-        seeds, n, stride = [5, 300, 7, 2**40 + 3], 70001, 2 * 70001 + 6
+        seeds, n, stride = [5, 300, 7, 2**40 + 3, 62 | 1 << 56, 63 | 6 << 57], 70001, 2 * 70001 + 6
         m = torch.full((len(seeds) * stride,), 0xAB, dtype=torch.uint8, device="cuda")
         torch.cuda.synchronize()
         rx.synth_device_streams(seeds, 999, n, m.data_ptr(), stride)
@@ -1411,3 +1542,83 @@ def test_psd_device_api_and_errors(fmrx, orc):
         for bad in ((x, 500, 48000.0), (x[:100], 512, 48000.0), (x, 16384, 48000.0)):
             with pytest.raises(fmrx.FmrxError):
                 rx.estimate_psd(*bad)
+
+
+# ---- tuning knobs: no value of any accepted range changes the output; the rest is refused --------
+
+KNOB_SWEEP = {  # include/fmrx.h FMRX_KNOB_* accepted ranges, every value or a spread of them
+    "pll_spec": [0, 1], "pll_sat": [0, 1], "pll_pred": [0, 1, 2], "pll_pipe": [0, 1], "pll_idx": [0, 1, 2],
+    "pll_cnt": list(range(32)), "pll_stick": [0, 1], "stereo_chunks": [0, 1, 2, 3, 4, 5, 7, 8, 9, 16, 33, 64],
+    "stereo_head": [1, 2, 7, 8, 9, 16, 17, 63, 64], "stereo_tail": [1, 2, 8, 15, 16, 64],
+    "stereo_lead": [0, 1, 2, 3, 7, 64], "audio_defer": [0, 1, 2, 3, 4, 5, 9, 10, 64], "bpf_tile": [0, 1],
+}
+KNOB_RANGES = {"pll_spec": (0, 1), "pll_sat": (0, 1), "pll_pred": (0, 2), "pll_pipe": (0, 1), "pll_idx": (0, 2),
+               "stereo_chunks": (0, 64), "mono_split": (-1, 1023), "bpf_tile": (0, 1), "halo_kernel": (0, 1),
+               "pll_cnt": (0, 31), "pll_stick": (0, 1), "stereo_head": (1, 64), "stereo_lead": (0, 64),
+               "audio_defer": (0, 64), "stereo_tail": (1, 64), "pll_inject": (-1, 1 << 30),
+               "pll_pipe_miss": (-(1 << 30), 1 << 30), "pll_hint_skew": (-16777216.0, 16777216.0)}
+
+
+def _at_trig(rx, ns, trig):
+    """Put every stream's PLL at trigOffset `trig` through the state blob (the runner regimes)."""
+    blob = bytearray(rx.get_state())
+    hdr = np.frombuffer(bytes(blob[:40]), np.uint32)
+    off = 40 + ns * (int(hdr[6]) + 4 * int(hdr[7]) + 4 * 64)
+    pll = np.frombuffer(bytes(blob[off: off + ns * 32]), np.float32).reshape(ns, 8).copy()
+    pll[:, 5] = trig
+    blob[off: off + ns * 32] = pll.tobytes()
+    rx.set_state(bytes(blob))
+
+
+def test_knob_sweep_bit_exact(fmrx, orc):
+    """Every tuning knob (api.cpp kKnobs) over its accepted range, one at a time, through
+    fmrx_debug_set_knob: a 20-stream 40-block stereo call from power-on (the pipelined engine:
+    chunking, deferral, band-pass form) against the oracle, the same call with every stream's PLL put
+    at trigOffset 2^19 - 6,000 and at 2^22 - 6,000 (the count / index / three-wave runners, their
+    handovers) against the default knobs' output there, and a 20-stream mono call (mono_split,
+    halo_kernel) against the oracle: bit-exact for every value."""
+    ns, nb, bb = 20, 40, 12800
+    ins = np.stack([iqgen.make("synth:%d" % (880 + s), nb * bb) for s in range(ns)])
+    want = np.stack([orc.run(0, 51, ins[s], ["pcm"])["pcm"] for s in range(ns)])
+    want_m = np.stack([orc.run(0, 51, ins[s], ["pcm_mono"])["pcm_mono"] for s in range(ns)])
+
+    def stereo(knobs, trig=None):
+        with fmrx.Receiver(0, fmrx.STEREO, n_streams=ns, knobs=knobs) as rx:
+            if trig is not None:
+                rx.process(ins[:, : 2 * bb])
+                _at_trig(rx, ns, trig)
+            return rx.process(ins if trig is None else ins[:, 2 * bb:])
+
+    base = {t: stereo({}, t) for t in (524288.0 - 6000.0, 4194304.0 - 6000.0)}
+    for name, values in KNOB_SWEEP.items():
+        for v in values:
+            assert np.array_equal(stereo({name: v}), want), (name, v)
+            for t, b in base.items():
+                assert np.array_equal(stereo({name: v}, t), b), (name, v, t)
+    for name, values in (("mono_split", [-1, 0, 1, 330, 512, 660, 1023]), ("halo_kernel", [0, 1])):
+        for v in values:
+            with fmrx.Receiver(0, fmrx.MONO, n_streams=ns, knobs={name: v}) as rx:
+                assert np.array_equal(rx.process(ins), want_m), (name, v)
+
+
+def test_knob_out_of_range_refused(fmrx, monkeypatch):
+    """A value outside a knob's range (include/fmrx.h), a fraction for an integer knob, NaN or an
+    unknown knob: fmrx_debug_set_knob returns FMRX_EINVAL and the context keeps running; a bad
+    environment variable makes fmrx_create refuse the context."""
+    with fmrx.Receiver(0, fmrx.STEREO) as rx:
+        for name, (lo, hi) in KNOB_RANGES.items():
+            rx.set_knob(name, lo)
+            rx.set_knob(name, hi)
+            for bad in (lo - 1, hi + 1, float("nan")) + ((lo + 0.5,) if name != "pll_hint_skew" else ()):
+                with pytest.raises(fmrx.FmrxError) as e:
+                    rx.set_knob(name, bad)
+                assert e.value.code == fmrx.FMRX_EINVAL, (name, bad)
+        with pytest.raises(fmrx.FmrxError):
+            fmrx._check(fmrx.lib().fmrx_debug_set_knob(rx.h, 99, 0.0))
+    for var, val in (("FMRX_PLL_CNT", "32"), ("FMRX_AUDIO_DEFER", "-1"), ("FMRX_STEREO_HEAD", "0"),
+                     ("FMRX_PLL_SPEC", "yes"), ("FMRX_MONO_SPLIT", "1024")):
+        monkeypatch.setenv(var, val)
+        with pytest.raises(fmrx.FmrxError) as e:
+            fmrx.Receiver(0, fmrx.STEREO)
+        assert e.value.code == fmrx.FMRX_EINVAL and var in str(e.value), (var, val)
+        monkeypatch.delenv(var)

@@ -14,7 +14,7 @@ import pytest
 
 import iqgen
 import oracle
-from conftest import case_input, golden_cases, load_case, long_runs
+from conftest import case_input, golden_cases, load_case, long_runs, unlocked_runs
 
 
 def sha(a):
@@ -73,6 +73,19 @@ def test_oracle_matches_long_hashes(orc, name):
     out = orc.run(h["mode"], h["rf_taps"], iq, ["pcm", "pcm_mono", "pll_state"])
     assert sha(out["pcm"]) == h["pcm_sha256"]
     assert sha(out["pcm_mono"]) == h["pcm_mono_sha256"]
+
+
+@pytest.mark.parametrize("name", ["unlocked_m0_nopilot_80s", "unlocked_m2_synth_170b"])
+def test_oracle_matches_unlocked_hashes(orc, name):
+    """The C restatement on a PLL that never locks, past the trigOffset stick (~20 s each; the
+    other two unlocked fixtures, random bytes and heavy noise, matched too when they were made)."""
+    h = unlocked_runs()[name]
+    bb, rf_fs = oracle.MODES[h["mode"]][0], oracle.MODES[h["mode"]][3]
+    iq = iqgen.make(h["recipe"], h["n_blocks"] * bb, rf_fs)
+    assert sha(iq) == h["input_sha256"]
+    out = orc.run(h["mode"], h["rf_taps"], iq, ["pcm", "pll_state"])
+    assert sha(out["pcm"]) == h["pcm_sha256"]
+    assert np.array_equal(bits(out["pll_state"][-6:]), bits(np.asarray(h["pll_state_last"], np.float32)))
 
 
 def test_const128_is_silence(orc):
