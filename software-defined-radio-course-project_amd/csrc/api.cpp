@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -70,6 +71,39 @@ struct DevBuf {
     }
 };
 
+// Pinned host memory, mapped into the device's address space (hipHostMalloc: kernels read and
+// write it through the same pointer): the staging of the host-buffer entry points' small calls
+// (the reference's per-block seam, project.cpp:48-84 / 132-196): the input goes to the device by
+// DMA from it, the kernels write their output into it in place -- one copy operation on the stream
+// and one host memcpy each way.
+template <class T>
+struct PinnedBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    int ensure(size_t count) {
+        if (count <= n) return 0;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(count, 1) * sizeof(T), hipHostMallocDefault) !=
+            hipSuccess) {
+            p = nullptr;
+            return fail(FMRX_ENOMEM, "hipHostMalloc of %zu bytes failed", count * sizeof(T));
+        }
+        n = count;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+// calls up to this many input bytes go through the pinned staging (larger ones: device buffers
+// and hipMemcpyAsync, whose DMA beats kernels reading host memory at that size)
+constexpr size_t kPinnedCallBytes = (size_t)4 << 20;
+
 }  // namespace
 
 struct fmrx_ctx {
@@ -108,6 +142,7 @@ struct fmrx_ctx {
     // staging for the host-buffer entry points
     DevBuf<uint8_t> d_in;
     DevBuf<int16_t> d_out;
+    PinnedBuf<uint8_t> h_in, h_out;  // the small host calls' staging (kPinnedCallBytes)
     DevBuf<float> d_f32;
     DevBuf<float> d_scratch;
     DevBuf<double> d_pll_side;    // PLL side data of one segment (pll_side_doubles)
@@ -169,7 +204,9 @@ struct fmrx_ctx {
 
 namespace {
 
-constexpr int kAudioHist50 = 50;  // demod samples a resampler output reads before its base
+constexpr int kAudioHist50 = 50;
+// stereo calls of up to this many blocks a stream take launch_stereo_audio_small (modes 0/1)
+constexpr int kSmallAudioBlocks = 4;  // demod samples a resampler output reads before its base
 
 // Serialises the entry points of one context (rf and audio stages may be driven from two
 // threads, as project.cpp does; they share the context's stream and scratch buffers).
@@ -296,6 +333,9 @@ int mono_segments(const fmrx_ctx* c, long long n_if, int wg_per_cu = 0) {
     // leaves the rest of each CU's LDS and SIMDs to the PLL runners beside it)
     const long long target_wg = 256LL * (wg_per_cu > 0 ? wg_per_cu : mono_wg_per_cu(c->geo.rf_decim));
     long long segs = std::max<long long>(1, target_wg / std::max(1, c->cfg.n_streams));
+    // a call too short to fill the grid even at one chunk a segment (the per-block seam: 4-5
+    // chunks a stream) takes one chunk a segment: twice the chunks, but all of them at once
+    if ((long long)c->cfg.n_streams * chunks <= target_wg) return (int)std::max<long long>(1, chunks);
     segs = std::min(segs, std::max<long long>(1, chunks / 4));
     return (int)std::max<long long>(1, segs);
 }
@@ -425,7 +465,9 @@ int run_mono_audio(fmrx_ctx* c, const float* d_demod, size_t demod_stride, size_
 }
 
 // Stereo engine on c->d_demod (history in front, n_if new samples per stream).
-int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono) {
+// src (may be null): the call's new demod, n_if a stream contiguous, not yet in c->d_demod --
+// the band-pass kernel reads it from there (pinned host memory: no copy launch) and stores it.
+int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono, const float* src = nullptr) {
     const int ns = c->cfg.n_streams;
     const size_t n_if = n_blocks * c->geo.if_samples;
     int rc = c->d_channel.ensure(n_if * ns);
@@ -442,13 +484,17 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
     S.ch_c = c->ch.data();
     S.ca_c = c->ca.data();
     S.bp_taps = c->geo.bp_taps;
+    S.src = src;
     const int t_bp = c->stage_timer.begin(c->stream);
     if (launch_bpf_pair(S, ns, c->stream, c->knobs.bpf_tile != 0)) return fail(FMRX_EHIP, "band-pass launch failed");
     c->stage_timer.end(t_bp, kStBpf, 0.0, c->stream);
     // project.cpp:166: PLL(carrier, 19000, if_fs, 2, 0, 0.01, ...)
     if ((rc = c->d_pll_side.ensure(pll_side_doubles((int)n_if, ns)))) return rc;
+    // a call of a few blocks (the per-block seam): the NCO, audio, state carry and demod history in
+    // one launch after the PLL (launch_stereo_audio_small); longer calls: the parallel kernels
+    const bool small = c->geo.audio_up == 1 && n_blocks <= (size_t)kSmallAudioBlocks;
     if (launch_pll(c->d_carrier.p, (int)n_if, ns, n_if, 19000.0f, (float)c->geo.if_fs, 2.0f, 0.0f,
-                   0.01f, c->d_pll.p, c->d_pll_side.p, c->stream, c->hint(c->pll_trig), c->pll_stats)) {
+                   0.01f, c->d_pll.p, c->d_pll_side.p, c->stream, c->hint(c->pll_trig), c->pll_stats, !small)) {
         c->pll_trig.known = false;
         return fail(FMRX_EHIP, "PLL launch failed");
     }
@@ -471,6 +517,13 @@ int run_stereo_audio(fmrx_ctx* c, size_t n_blocks, int16_t* d_pcm, float* d_mono
     A.at = c->geo.audio_taps_total;
     A.audio_c = c->d_audio.p;
     const int t_au = c->stage_timer.begin(c->stream);
+    if (small) {
+        if (launch_stereo_audio_small(A, ns, pll_trig_args(c->d_pll_side.p, (int)n_if, ns), n_if, 2.0f, 0.0f,
+                                      c->d_pll.p, kDemodHist, c->stream))
+            return fail(FMRX_EHIP, "stereo audio launch failed");
+        c->stage_timer.end(t_au, kStAudio, 0.0, c->stream);
+        return 0;
+    }
     if (launch_stereo_audio(A, ns, c->stream)) return fail(FMRX_EHIP, "stereo audio launch failed");
     c->stage_timer.end(t_au, kStAudio, 0.0, c->stream);
     // demod history for the next call: last kDemodHist samples -> front, every stream in one
@@ -680,7 +733,10 @@ int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks,
         // profiles/r05/ab_audio_defer/); 2, the default, chunks 0 .. K - 2 beside the LAST chunk's
         // PLL only and chunk K - 1's after it: a short tail, one chunk's chains disturbed
         // (0.4058 -> 0.3955 s, profiles/r05/ab_audio_defer2/); 2 + e, chunks 0 .. e - 1 of those
-        // beside chunk K - 2's PLL instead (a shorter queue beside the last PLL)
+        // beside chunk K - 2's PLL instead (a shorter queue beside the last PLL).  Everything here is
+        // on s_audio in issue order, so NCO(K - 1) and audio(K - 1) queue behind all deferred audio
+        // stages (the intended tail); e is clamped to K - 2, so with K <= 3 the 2 + e forms are 2
+        // (same bits either way: only the order on s_audio changes)
         const int ad = c->knobs.audio_defer;
         const int early = ad >= 2 ? std::min(ad - 2, K - 2) : 0;
         if (ad == 0 && (rc = audio(k))) return rc;
@@ -972,6 +1028,7 @@ void fmrx_destroy(fmrx_ctx* c) {
     c->d_audio_hist.release(); c->d_demod.release(); c->d_channel.release(); c->d_carrier.release();
     c->d_pll.release(); c->d_mix_tail.release(); c->d_mono_state.release(); c->d_in.release();
     c->d_out.release(); c->d_f32.release(); c->d_scratch.release(); c->d_sintab.release();
+    c->h_in.release(); c->h_out.release();
     c->d_pll_side.release(); c->d_pll_side2.release();
     c->d_rds_taps.release(); c->d_rds_dhist.release(); c->d_rds_chan.release(); c->d_rds_car.release();
     c->d_rds_pll.release();
@@ -1194,6 +1251,24 @@ int fmrx_kernel_timing(fmrx_ctx* c, int reset, double* avg_ms, long* launches) {
 }
 
 // ---- host-buffer entry points ---------------------------------------------------------------
+// End of a small host call: poll the stream instead of hipStreamSynchronize, whose blocking wait
+// wakes the thread ~10 us after the last kernel of a 20-80 us call (the per-block seam's
+// calls); after kSpinNs the call is not small after all and blocks.
+constexpr long long kSpinNs = 2000000;
+int wait_small(fmrx_ctx* c) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0;; k++) {
+        const hipError_t e = hipStreamQuery(c->stream);
+        if (e == hipSuccess) return FMRX_OK;
+        if (e != hipErrorNotReady) return fail(FMRX_EHIP, "stream query: %s", hipGetErrorString(e));
+        if ((k & 63) == 63 && std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                  std::chrono::steady_clock::now() - t0).count() > kSpinNs)
+            break;
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return FMRX_OK;
+}
+
 int fmrx_process(fmrx_ctx* c, const uint8_t* iq, size_t n_blocks, int16_t* pcm) {
     CtxLock lock_(c);
     if (!c || !iq || !pcm) return fail(FMRX_EINVAL, "null argument");
@@ -1203,6 +1278,17 @@ int fmrx_process(fmrx_ctx* c, const uint8_t* iq, size_t n_blocks, int16_t* pcm) 
     const size_t ns = c->cfg.n_streams;
     const size_t in_bytes = ns * n_blocks * c->geo.block_bytes;
     const size_t out_n = ns * n_blocks * c->geo.pcm_samples;
+    if (in_bytes <= kPinnedCallBytes) {  // pinned staging: the input by DMA, the PCM written in place
+        if ((rc = c->h_in.ensure(in_bytes)) || (rc = c->h_out.ensure(out_n * sizeof(int16_t))) ||
+            (rc = c->d_in.ensure(in_bytes)))
+            return rc;
+        std::memcpy(c->h_in.p, iq, in_bytes);
+        HIPCHK(hipMemcpyAsync(c->d_in.p, c->h_in.p, in_bytes, hipMemcpyHostToDevice, c->stream));
+        if ((rc = fmrx_process_device(c, c->d_in.p, n_blocks, reinterpret_cast<int16_t*>(c->h_out.p)))) return rc;
+        if ((rc = wait_small(c))) return rc;
+        std::memcpy(pcm, c->h_out.p, out_n * sizeof(int16_t));
+        return FMRX_OK;
+    }
     if ((rc = c->d_in.ensure(in_bytes)) || (rc = c->d_out.ensure(out_n))) return rc;
     HIPCHK(hipMemcpyAsync(c->d_in.p, iq, in_bytes, hipMemcpyHostToDevice, c->stream));
     if ((rc = fmrx_process_device(c, c->d_in.p, n_blocks, c->d_out.p))) return rc;
@@ -1221,6 +1307,19 @@ int fmrx_rf_block(fmrx_ctx* c, const uint8_t* iq, size_t n_blocks, float* demod)
     const size_t ns = c->cfg.n_streams;
     const size_t in_bytes = ns * n_blocks * c->geo.block_bytes;
     const size_t n_if = n_blocks * c->geo.if_samples;
+    if (in_bytes <= kPinnedCallBytes) {  // pinned staging: the input by DMA (the fused kernel's
+                                         // staging reads host memory 4x slower), the demod in place
+        if ((rc = c->h_in.ensure(in_bytes)) || (rc = c->h_out.ensure(sizeof(float) * ns * n_if)) ||
+            (rc = c->d_in.ensure(in_bytes)))
+            return rc;
+        std::memcpy(c->h_in.p, iq, in_bytes);
+        HIPCHK(hipMemcpyAsync(c->d_in.p, c->h_in.p, in_bytes, hipMemcpyHostToDevice, c->stream));
+        float* h_demod = reinterpret_cast<float*>(c->h_out.p);
+        if ((rc = run_fused(c, c->d_in.p, n_blocks, nullptr, nullptr, h_demod, n_if, 0, false))) return rc;
+        if ((rc = wait_small(c))) return rc;
+        std::memcpy(demod, h_demod, sizeof(float) * ns * n_if);
+        return FMRX_OK;
+    }
     if ((rc = c->d_in.ensure(in_bytes)) || (rc = c->d_f32.ensure(ns * n_if))) return rc;
     HIPCHK(hipMemcpyAsync(c->d_in.p, iq, in_bytes, hipMemcpyHostToDevice, c->stream));
     if ((rc = run_fused(c, c->d_in.p, n_blocks, nullptr, nullptr, c->d_f32.p, n_if, 0, false))) return rc;
@@ -1239,21 +1338,44 @@ int fmrx_audio_block(fmrx_ctx* c, const float* demod, size_t n_blocks, int16_t* 
     const size_t ns = c->cfg.n_streams;
     const size_t n_if = n_blocks * c->geo.if_samples;
     const size_t out_n = ns * n_blocks * c->geo.pcm_samples;
-    if ((rc = c->d_out.ensure(out_n))) return rc;
+    if (c->cfg.channels == FMRX_MONO && c->audio_hist_stale)
+        return fail(FMRX_ESTATE, "no audio history after fmrx_seek (run a fused call first)");
+    // small calls: the demod through the pinned staging (stereo: read there by the band-pass
+    // kernel; mono: one copy), the PCM written by the audio kernel into pinned memory in place
+    const bool pinned = sizeof(float) * ns * n_if <= kPinnedCallBytes;
+    const float* src = demod;
+    int16_t* d_pcm = nullptr;
+    if (pinned) {
+        if ((rc = c->h_in.ensure(sizeof(float) * ns * n_if)) || (rc = c->h_out.ensure(out_n * sizeof(int16_t))))
+            return rc;
+        std::memcpy(c->h_in.p, demod, sizeof(float) * ns * n_if);
+        src = reinterpret_cast<const float*>(c->h_in.p);
+        d_pcm = reinterpret_cast<int16_t*>(c->h_out.p);
+    } else {
+        if ((rc = c->d_out.ensure(out_n))) return rc;
+        d_pcm = c->d_out.p;
+    }
     if (c->cfg.channels == FMRX_MONO) {
-        if (c->audio_hist_stale) return fail(FMRX_ESTATE, "no audio history after fmrx_seek (run a fused call first)");
         if ((rc = c->d_f32.ensure(ns * n_if))) return rc;
-        HIPCHK(hipMemcpyAsync(c->d_f32.p, demod, sizeof(float) * ns * n_if, hipMemcpyHostToDevice, c->stream));
-        if ((rc = run_mono_audio(c, c->d_f32.p, n_if, n_if, c->d_out.p, nullptr))) return rc;
+        HIPCHK(hipMemcpyAsync(c->d_f32.p, src, sizeof(float) * ns * n_if, hipMemcpyHostToDevice, c->stream));
+        if ((rc = run_mono_audio(c, c->d_f32.p, n_if, n_if, d_pcm, nullptr))) return rc;
     } else {
         if ((rc = ensure_demod(c, n_if))) return rc;
-        HIPCHK(hipMemcpy2DAsync(c->d_demod.p + kDemodHist, c->demod_stride * sizeof(float), demod,
-                                n_if * sizeof(float), n_if * sizeof(float), ns,
-                                hipMemcpyHostToDevice, c->stream));
-        if ((rc = run_stereo_audio(c, n_blocks, c->d_out.p, nullptr))) return rc;
+        if (!pinned)
+            HIPCHK(hipMemcpy2DAsync(c->d_demod.p + kDemodHist, c->demod_stride * sizeof(float), src,
+                                    n_if * sizeof(float), n_if * sizeof(float), ns,
+                                    hipMemcpyHostToDevice, c->stream));
+        // pinned: the band-pass kernel reads the staging buffer itself (one launch fewer)
+        if ((rc = run_stereo_audio(c, n_blocks, d_pcm, nullptr, pinned ? src : nullptr))) return rc;
     }
-    HIPCHK(hipMemcpyAsync(pcm, c->d_out.p, out_n * sizeof(int16_t), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    if (!pinned)
+        HIPCHK(hipMemcpyAsync(pcm, c->d_out.p, out_n * sizeof(int16_t), hipMemcpyDeviceToHost, c->stream));
+    if (pinned) {
+        if ((rc = wait_small(c))) return rc;
+        std::memcpy(pcm, c->h_out.p, out_n * sizeof(int16_t));
+    } else {
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
     return FMRX_OK;
 }
 

@@ -41,6 +41,9 @@ struct StereoLaunch {
     const float* ch_c;      // bp taps, HOST memory (passed to the kernel by value)
     const float* ca_c;
     int bp_taps;
+    const float* src = nullptr;  // non-null (tiled kernel only): the call's n_if new demod samples a
+                                 //   stream (stride n_if, e.g. pinned host memory) are read from here
+                                 //   and written into demod behind the history -- no separate copy
 };
 // tiled = false: the per-output kernel (A/B measurements; same bits)
 int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s, bool tiled = true);
@@ -186,6 +189,13 @@ int launch_pll_cnt(hipStream_t s, const float* io, int n, int n_streams, size_t 
 // not demoted), which this kernel clears.  One stream a workgroup: a speculative chain
 // (pll_spec_lane_kernel's step) checked a sub-segment behind by the other waves, which also form
 // its side data; a batch that does not verify is recomputed exactly and the chain resumes after it.
+// steps an interval of launch_pll's form (17-23) on the count runner (cnt) or the index / three-wave
+// runner: a range of fewer than 24 intervals cannot demote (launch_pll skips pll_demoted_kernel)
+int pll_form_interval(int form, bool cnt);
+// launch_pll: a call of fewer steps a stream than kPllShortCall runs only 16-step forms; a range of
+// fewer than kPllShortIntervals long intervals too; a long form's tail past its last whole interval
+// of at least kPllShortTail steps runs on the 16-step form (three 16-step intervals)
+constexpr size_t kPllShortCall = 4096, kPllShortIntervals = 4, kPllShortTail = 48;
 int launch_pll_demoted(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step,
                        float norm_bw, float* st, float* out, size_t ostride, int inject, unsigned long long* stats);
 // fmrx_debug_pll_redos: per stream kPllRedoSlots u32, by the trigOffset range r of the runner's
@@ -223,6 +233,13 @@ struct AudioLaunch {
 // last block.  launch_stereo_audio: all of them.
 int launch_stereo_audio_range(const AudioLaunch& L, int b0, int b1, bool last, int n_streams, hipStream_t s);
 int launch_stereo_audio(const AudioLaunch& L, int n_streams, hipStream_t s);
+// A few blocks a stream in ONE launch (modes 0/1, the per-block seam): the NCO from the PLL's
+// trigArgs (args, astride floats a stream: pll_trig_args of a launch_pll with nco = false), the audio
+// of every block in order, the state carry and the demod history move (the last demod_hist samples
+// of the call to the front of its buffer); -1 when the geometry does not fit the tile.
+const float* pll_trig_args(const double* side, int n, int n_streams);
+int launch_stereo_audio_small(const AudioLaunch& L, int n_streams, const float* args, size_t astride, float nco_scale,
+                              float phase_adjust, float* pll_st, int demod_hist, hipStream_t s);
 
 // ---- RDS front half (project.cpp:200-271) ----------------------------------------------
 constexpr int kRdsTaps = 51;        // bp_taps, project.cpp:307

@@ -80,6 +80,9 @@ constexpr int kPllBatch = 16;
 // instead of paying a failed interval plus its redo each time.  Locked streams miss <= ~1 % of
 // intervals (profiles/r05 redos); unlocked ones 75-100 % (profiles/r06/unlocked.json).
 constexpr int kPllDemoteMisses = 24;
+// only a runner launch of at least this many intervals demotes (launch_pll queues the demoted kernel
+// after exactly those: a shorter range cannot pay for it, e.g. the per-block seam's 640 steps)
+constexpr int kPllDemoteMinIntervals = 64;
 // test hook (knob pll_pipe_miss = m): m >= 1 a forced miss on interval m (past the last: the last),
 // m <= -2 on every interval from -m - 1 on (an unlocked loop's pattern: the demotion runs), -1 off
 __device__ inline bool pll_hook_miss(int i, int miss, int ni) {

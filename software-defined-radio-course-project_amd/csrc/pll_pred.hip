@@ -31,6 +31,7 @@
 // the result is the certified path's bit for bit whatever was predicted.
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <type_traits>
@@ -568,11 +569,22 @@ __device__ __noinline__ float exact_e(float a, float v) {
     return e;
 }
 
+// The e of a range's first step from the state it starts with (pll_step's first half with the
+// state's own feedback, no sincos context: the library atan2, as pll_redo's first step).
+__device__ __noinline__ float exact_e_fb(float fbI, float fbQ, float v) {
+    const DeviceLib lib;
+    const float eI = v * fbI;
+    const float eQ = v * (-fbQ);
+    return lib.atan2f_(eQ, eI);
+}
+
 // One wave a SIMD (amdgpu_waves_per_eu): the register budget is the chain's, so the scheduler
 // keeps each burst of reads whole instead of threading it through the steps for occupancy.
 // io / out: the stream's input and trigArg rows from the range's first sample (stride / ostride
 // floats a stream), n samples; st: the state (read at the start, the exact end state written).
-template <int NB, int BPI, int RD, int NC, bool STK = false>
+// WIDE (the short-call form, launch_pll_pipe form 24): the 16-step five-candidate form from 2^20 on,
+// across the later forms' ranges and the stick (five candidates cover what three do there)
+template <int NB, int BPI, int RD, int NC, bool STK = false, bool WIDE = false>
 __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))) pll_pipe_kernel(const float* io, int n, int n_streams, size_t stride,
                                                       double step, float norm_bw, float* st, float* out_base,
                                                       size_t ostride, int inject, int miss,
@@ -596,7 +608,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
 #endif
     constexpr int CHM = FMRX_CHM;
     constexpr int CH = NC == 5 ? 16 : (NI < CHM ? NI : CHM);
-    // rings of four intervals (interval k in slot k & 3; interval 0 is batch 0), per step: NC = 3:
+    // rings of four intervals (interval k in slot k & 3; slot 0 holds the range's start state), per step: NC = 3:
     // the thresholds of c0 and c0 + 1 ulp and the e of c0 - 1 and c0 (sel), the e of c0 + 1
     // (sep); NC = 5: the thresholds of c0 - 1 .. c0 + 2 (sel), the e of c0 - 2 .. c0 + 1 (sel2),
     // of c0 + 2 (sep); bits(c0) - HC (scb), P (spr); the certification of each candidate's e
@@ -645,7 +657,9 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     PllState p{uni(S[0]), uni(S[1]), uni(S[2]), uni(S[3]), uni(S[5])};
     // the variant's domain (uniform over the group): NC = 3 from 2^22; NC = 5 with 64-step
     // intervals in [2^21, 2^22), with 16-step ones in [2^20, 2^21)
+    static_assert(!WIDE || (NC == 5 && BPI == 1 && !STK), "the wide form is the 16-step five-candidate one");
     const bool in_domain = STK ? pll_pipe_stream(p.trig, step, kPllTrigStick)
+                         : WIDE ? pll_pipe_stream(p.trig, step, kPllPipeMinLow)
                          : NC == 3 ? pll_pipe_stream(p.trig, step, kPllPipeMin)
                                    : NI >= 64 ? pll_pipe_stream(p.trig, step, kPllPipeMin5, kPllPipeMin - 1.0f)
                                               : pll_pipe_stream(p.trig, step, kPllPipeMinLow, kPllPipeMin5 - 1.0f);
@@ -656,7 +670,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         return step * (double)(float)fmin(t0d + (double)(j + 1), (double)kPllTrigStick);
     };
     const int nb = n / NB;
-    const int ni = nb > 0 ? (nb - 1) / BPI : 0;  // intervals after batch 0
+    const int ni = nb / BPI;  // intervals 1 .. ni from the range's first step (the first predicted too)
     // test hook: a miss on interval 1 + (inject + s) % ni of this stream (the exact redo runs)
     const int inj = inject >= 0 && ni > 0 ? 1 + (inject + s) % ni : -1;
     // steps [j0, j1) exactly from state q (c): outputs
@@ -685,7 +699,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         }
         return;
     }
-    auto j0 = [](int k) { return NB + (k - 1) * NI; };  // interval k's first step (k >= 1)
+    auto j0 = [](int k) { return (k - 1) * NI; };  // interval k's first step (k >= 1)
 
     if (w > 0) {
         // ring of RD intervals of step inputs, interval k in slot k % RD, loaded RD - 1 ahead
@@ -807,7 +821,9 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
                     ca2 = sel2[NC == 5 ? sl : 0][NC == 5 ? NB * gb - 1 : 0];
                 } else if (sexact[(k - 1) & 3]) {
                     const int j = j0(k);
-                    const float e = exact_e((float)(pr_at(j - 1) + (double)ph), x[min(j, n - 1)]);
+                    // (interval 1: the range's first step, from the state's own feedback)
+                    const float e = k == 1 ? exact_e_fb(p.fbI, p.fbQ, x[0])
+                                           : exact_e((float)(pr_at(j - 1) + (double)ph), x[min(j, n - 1)]);
                     ca = NC == 3 ? make_float4(0.0f, 0.0f, e, e) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                     ca2 = make_float4(e, e, e, e);
                     cep = e;
@@ -946,9 +962,8 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
 
     // ---- the chain
-    PllCtx ctx{};
-    ctx.valid = false;
-    exact(p, ctx, 0, NB);  // batch 0 on the exact path (see pll_spec_kernel)
+    // interval 1 starts at the range's first step, predicted from the start phase like every other
+    // (until round 6 its first batch ran on the exact path: 16 steps at ~400 ns, ~6 us a launch)
     float integ = p.integ, phase = p.phase;
     // (Ki, Kp) as an SGPR pair for the chain's v_pk_mul_f32 (uniform: readfirstlane)
     const uint64_t kk = (uint64_t)__builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, Ki)) |
@@ -963,7 +978,12 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
         carry2 = make_float4(e, e, e, e);
         carry_ep = e;
     };
-    carry_exact((float)ctx.x, 1);
+    {  // step 0's e from the state's feedback (the exact path's first step)
+        const float e = exact_e_fb(p.fbI, p.fbQ, x[0]);
+        carry = NC == 3 ? make_float4(0.0f, 0.0f, e, e) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        carry2 = make_float4(e, e, e, e);
+        carry_ep = e;
+    }
     if (t == 0) {
         sst[0][BPI - 1] = make_float2(integ, phase);  // the start of interval 1 (the evaluators' interval 2)
 #pragma unroll
@@ -980,6 +1000,20 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     PllState qd;        // demoted: the exact state at the end of the redone interval, and its step
     PllCtx cd{};
     long long jd = 0;
+    // the exact state before interval f from the ring (its trigArg's sin / cos recomputed); before
+    // interval 1 the range's start state as given (its feedback may not be that sin / cos: a state
+    // set by the caller)
+    auto state_before = [&](int f, PllState& q, PllCtx& c) {
+        if (f <= 1) {
+            q = p;
+            c = PllCtx{};
+            c.valid = false;
+            return;
+        }
+        const float2 r0 = sst[(f - 1) & 3][BPI - 1];
+        const float a = (float)(pr_at(j0(f) - 1) + (double)r0.y);  // the trigArg before it
+        pll_state_at(q, c, r0.x, r0.y, trig0, (long long)j0(f), a, DeviceLib{});
+    };
     // interval i on the fast chain from (integ, phase) and the carry, its data in ring slot i & 3
     auto run = [&](int i) {
         const int is = i & 3;
@@ -1079,13 +1113,11 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             n_inj += inj == i - 2 ? 1 : 0;  // the inject hook's interval, redone exactly
             __syncthreads();  // B1: E2's stores of interval i - 1 happen before the redo's
             // interval i - 2 (missed) exactly, from the state at its start (the end of interval
-            // i - 3 in the ring; interval 0 is batch 0, slot 0 holds its end)
+            // i - 3 in the ring; interval 1: the range's own start state, slot 0)
             const int f = i - 2;
-            const float2 r0 = sst[(f - 1) & 3][BPI - 1];
-            const float a = (float)(pr_at(j0(f) - 1) + (double)r0.y);  // the trigArg before it
             PllState q;
             PllCtx c{};
-            pll_state_at(q, c, r0.x, r0.y, trig0, (long long)j0(f), a, DeviceLib{});
+            state_before(f, q, c);
             exact(q, c, j0(f), j0(f) + NI);
             if (t == 0) {
                 sst[f & 3][BPI - 1] = make_float2(q.integ, q.phase);
@@ -1094,7 +1126,8 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             }
             integ = q.integ;
             phase = q.phase;
-            if (over) {  // demoted: the evaluators leave after B1.5, pll_demoted_kernel runs the rest
+            if (over && n >= kPllDemoteMinIntervals * NI) {  // demoted: the evaluators leave after B1.5,
+                                                               // pll_demoted_kernel runs the rest
                 sdemote = 1;
                 __syncthreads();  // B1.5
                 demoted = true;
@@ -1124,18 +1157,15 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     if (demoted) {  // the redone interval's exact end: pll_demoted_kernel runs the rest
         q = qd;
         c = cd;
-        f = (int)((jd - NB) / NI) + 1;
+        f = (int)(jd / NI) + 1;
         n_dem = (unsigned long long)(n - jd);
     } else {
         __syncthreads();  // E2's checks of the last two intervals
         // a miss in them: from the first missed interval on exactly; then the steps past the last
         // interval exactly, from the state at the end of the last good interval
         f = smiss[(ni - 1) & 3] ? ni - 1 : (smiss[ni & 3] ? ni : ni + 1);
-        const float2 r0 = sst[(f - 1) & 3][BPI - 1];
-        const long long jf = j0(f);
-        const float a = (float)(pr_at(jf - 1) + (double)r0.y);
-        pll_state_at(q, c, r0.x, r0.y, trig0, jf, a, DeviceLib{});
-        exact(q, c, jf, n);
+        state_before(f, q, c);
+        exact(q, c, j0(f), n);
     }
     if (t == 0) {
         S[0] = q.integ; S[1] = q.phase; S[2] = q.fbI; S[3] = q.fbQ; S[5] = q.trig;
@@ -1148,9 +1178,9 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             atomicAdd(stats + 1, (unsigned long long)nb);
         }
         // fmrx_debug_pll_redos: this stream's redone intervals and demoted steps
-        if (redos) {  // by the range's trigOffset (1: the 16-step five-candidate form, 2: the 64/128-step
-                      // one, 3: three candidates and the stick)
-            const int rg = NI == 16 ? 1 : NC == 5 ? 2 : 3;
+        if (redos) {  // by the range's trigOffset at its start (the wide 16-step form runs in any
+                      // range from 2^20: launch_pll's short calls and long forms' tails)
+            const int rg = pll_redo_range(trig0);
             atomicAdd(&redos[kPllRedoSlots * (size_t)s + rg], (unsigned)n_redo);
             atomicAdd(&redos[kPllRedoSlots * (size_t)s + 4 + rg], (unsigned)n_dem);
         }
@@ -1225,9 +1255,8 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
     __shared__ float4 sp[4][NI];
     __shared__ float se[4][NR][64];
     __shared__ int srow[4][NI];
-    __shared__ float2 sst[4];
+    __shared__ float4 sst[4];  // (integ, phase, the verdict "redone exactly" as int bits, -)
     __shared__ int sexact[4];
-    __shared__ int sdemote;  // the interval after which the chain left (pll_demote), or 0
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
     const int s = blockIdx.x;  // grid = n_streams
     const float* x = io + (size_t)s * stride;
@@ -1244,7 +1273,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         return step * (double)(float)fmin(t0d + (double)(j + 1), (double)kPllTrigStick);
     };
     const int nb = n / NI;
-    const int ni = nb > 0 ? nb - 1 : 0;  // intervals after interval 0 (exact)
+    const int ni = nb;  // intervals 1 .. nb from the range's first step (the first predicted too)
     // test hook: a forced miss on interval 1 + (inject + s) % ni (counted as resumed)
     const int inj = inject >= 0 && ni > 0 ? 1 + (inject + s) % ni : -1;
     auto exact = [&](PllState& q, PllCtx& c, long long j0, long long j1) {
@@ -1270,7 +1299,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         }
         return;
     }
-    auto j0 = [](int k) { return NI * k; };  // interval k's first step
+    auto j0 = [](int k) { return NI * (k - 1); };  // interval k's first step (k >= 1)
 
     if (w > 0) {
         // this wave's rows r = w - 1 + NW q; lane t: step J = r SPP + t / NC, candidate t % NC
@@ -1309,6 +1338,12 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
                 }
             }
         };
+        // test hook pll_pipe_miss = -m (m >= 2): every interval from m - 1 on misses -- its step-0
+        // base moved off the candidates, so the chain's lane index leaves the row (wave 1, lane 0)
+        auto hook_poison = [&](int k) {
+            if (miss <= -2 && k >= -miss - 1 && w == 1 && t == 0)
+                reinterpret_cast<uint32_t*>(&sp[k & 3][0])[2] += 0x40000000u;
+        };
         // wave 1: interval k's trigArgs, base + the chain's lane index (the chain stored a redone
         // interval itself)
         auto store = [&](int k) {
@@ -1321,34 +1356,33 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         };
 #pragma unroll
         for (int u = 0; u < RD; u++) ld(1 + u, vq[(1 + u) % RD]);
-        put(1, p.phase, vq[1 % RD]);  // interval 1 from the phase at interval 0's start
+        put(1, p.phase, vq[1 % RD]);  // interval 1 from the start phase (its own start)
+        hook_poison(1);
         ld(1 + RD, vq[1 % RD]);
         __syncthreads();  // (prologue)
         unsigned long long ev_body = 0, ev_wait = 0;
-        // the chain demoted the stream (pll_demote) after redoing interval i - 1 itself: it runs the
-        // rest of the range alone, no barrier is reached any more
-        bool demoted = false;
-        for (int i0 = 1; i0 <= ni && !demoted; i0 += RD) {
+        // pll_demote is the chain's (its verdicts are at hand there, a few scalar ops an interval):
+        // when it leaves after interval i - 1 it says so in that interval's state word (w), and the
+        // evaluators store that interval's trigArgs and leave too, without another barrier
+        bool left = false;
+        for (int i0 = 1; i0 <= ni && !left; i0 += RD) {
             unroll_ic(
                 [&](auto uc) {
                     constexpr int u = decltype(uc)::value;
                     constexpr int sl = (2 + u) % RD;  // slot of interval i + 1
                     const int i = i0 + u;
-                    if (i <= ni && !demoted) {
-                        // once a group of RD intervals: has the chain left (pll_demote) after an
-                        // interval before this one?  sdemote names it; the chain takes the barriers
-                        // of the intervals in between (those evaluations and stores are wasted and
-                        // the rest of the range is pll_demoted_kernel's, which rewrites them)
-                        if (u == 0 && !kAbNoDemote) {
-                            const int dm = __builtin_amdgcn_readfirstlane(sdemote);
-                            if (dm != 0 && dm < i) {
-                                demoted = true;
-                                return;
-                            }
-                        }
+                    if (i <= ni && !left) {
                         const unsigned long long p0 = PROF_T();
+                        // the chain's state at interval i's start (and whether it left there)
+                        const float4 rs = sst[(i - 1) & 3];
+                        if (!kAbNoDemote && __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, rs.w)) != 0) {
+                            store(i - 1);
+                            left = true;
+                            return;
+                        }
                         if (i + 1 <= ni) {
-                            put(i + 1, sst[(i - 1) & 3].y, vq[sl]);  // from the phase at interval i's start
+                            put(i + 1, rs.y, vq[sl]);  // from the phase at interval i's start
+                            hook_poison(i + 1);
                             ld(i + 1 + RD, vq[sl]);
                         }
                         store(i - 1);
@@ -1360,7 +1394,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
                 },
                 std::make_integer_sequence<int, RD>{});
         }
-        if (!demoted) store(ni);
+        if (!left) store(ni);
 #ifdef FMRX_AB_PROF
         if (t == 0 && w == 1) {
             atomicAdd(&g_idx_prof[2], ev_body);
@@ -1373,9 +1407,8 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
     }
 
     // ---- the chain
-    PllCtx ctx{};
-    ctx.valid = false;
-    exact(p, ctx, 0, NI);  // interval 0 on the exact path
+    // interval 1 starts at the range's first step, predicted from the start phase like every other
+    // (until round 6 a whole interval ran first on the exact path, at ~400 ns a step)
     float integ = p.integ, phase = p.phase;
     // the carry: the candidate row value of the previous trigArg and its lane (SGPR); after an
     // exact stretch that trigArg's exact e in every lane
@@ -1385,21 +1418,30 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         cE = exact_e(a, x[min(j0(k), n - 1)]);
         cL = 0;
     };
-    carry_exact((float)ctx.x, 1);
+    cE = exact_e_fb(p.fbI, p.fbQ, x[0]);  // step 0's e from the state's feedback (every lane)
     if (t == 0) {
-        sst[0] = make_float2(integ, phase);
+        // the start state; its verdict (z) reads as a hit (no prediction pll_demote counts), and
+        // no i >= 2 test in the evaluators' loop (LLVM peels a whole unrolled iteration for one)
+        sst[0] = make_float4(integ, phase, 0.0f, 0.0f);
         sexact[0] = 1;
-        sdemote = 0;
     }
     __syncthreads();  // (prologue)
-    uint32_t hist = 0;  // the last 32 intervals' verdicts (pll_demote)
-    int dem_i = 0;      // the interval after which the chain left (pll_demote), or 0
+    // pll_demote: the chain's verdicts of its last 32 intervals (SGPR bits); past kPllDemoteMisses
+    // misses it leaves after the interval (dem_i) and the demoted kernel runs the rest
+    int dem_i = 0;
+    uint32_t hist = 0;
     unsigned long long n_redo = 0, n_inj = 0, ch_body = 0, ch_wait = 0;
     const uint32_t off = (uint32_t)(NC * ((t & (NI - 1)) % SPP));  // lane t's step's lane offset
-    for (int i = 1; i <= ni; i++) {
+    uint32_t prev_bad = 0;  // the last interval's verdict (SGPR)
+    for (int i = 1; i <= ni && dem_i == 0; i++) {
         const unsigned long long p0 = PROF_T();
         const int is = i & 3;
         const float integ0 = integ, phase0 = phase;
+        // the verdicts up to interval i - 1 decide whether the chain leaves after this one: scalar
+        // work at the interval's start, off the chain's path (at its end it delayed the barrier)
+        hist = (hist << 1) | prev_bad;
+        const bool leave = !kAbNoDemote && i < ni && n >= kPllDemoteMinIntervals * NI &&
+                           __builtin_popcount(hist) >= kPllDemoteMisses;
         // the interval's data before its steps (NI 16-byte broadcasts, NR row reads)
         float4 D[NI];
         float E[NR];
@@ -1433,42 +1475,32 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         // taken (the phase), the start state in pll_batch_fast's range; test hooks force misses
         const bool lane_bad = t < NI && (uint32_t)row - off >= (uint32_t)NC;
         const bool bad = __builtin_amdgcn_ballot_w64(lane_bad) != 0 || !(phase == phase) ||
-                         !(fabsf(phase0) < kPllMaxPhase && fabsf(integ0) < kPllMaxInteg) || pll_hook_miss(i, miss, ni) || i == inj;
+                         !(fabsf(phase0) < kPllMaxPhase && fabsf(integ0) < kPllMaxInteg) || i == min(miss, ni) ||
+                         i == inj;
         if (bad) {  // uniform: redo the interval exactly from its start (the chain stores it)
             n_redo++;
             n_inj += i == inj ? 1 : 0;
-            const float a = (float)(pr_at(j0(i) - 1) + (double)phase0);  // the trigArg before it
-            PllState q;
+            PllState q = p;  // interval 1: the range's start state as given
             PllCtx c{};
-            pll_state_at(q, c, integ0, phase0, trig0, (long long)j0(i), a, DeviceLib{});
+            c.valid = false;
+            if (i > 1) {
+                const float a = (float)(pr_at(j0(i) - 1) + (double)phase0);  // the trigArg before it
+                pll_state_at(q, c, integ0, phase0, trig0, (long long)j0(i), a, DeviceLib{});
+            }
             exact(q, c, j0(i), j0(i) + NI);
             integ = q.integ;
             phase = q.phase;
             carry_exact((float)c.x, i + 1);
         }
         if (t < NI) srow[is][t] = row;
-        // demoted right after a redo (this interval's trigArgs are stored): the evaluators read
-        // sdemote at the top of their next group of intervals
-        // (bad is uniform but VGPR-derived: taken through an SGPR, so hist, the demotion and the
-        // loop exit stay scalar -- a divergent exit would turn the whole interval loop into a
-        // masked one, measured ~4 ns a step slower on the index forms)
-        const bool bad_u = __builtin_amdgcn_readfirstlane((int)bad) != 0;
-        const bool dem = !kAbNoDemote && pll_demote(hist, bad_u) && bad_u && i < ni;
-        sst[is] = make_float2(integ, phase);
+        prev_bad = (uint32_t)__builtin_amdgcn_readfirstlane(bad ? 1 : 0);  // (scalar: no divergent loop)
+        sst[is] = make_float4(integ, phase, __builtin_bit_cast(float, bad ? 1 : 0), __builtin_bit_cast(float, leave ? 1 : 0));
         sexact[is] = bad ? 1 : 0;
-        if (dem) sdemote = i;
         const unsigned long long p1 = PROF_T();
         __syncthreads();
         ch_body += p1 - p0;
         ch_wait += PROF_T() - p1;
-        if (dem) {
-            dem_i = i;
-            // the evaluators' barriers up to the top of their next group of RD intervals (from
-            // interval 1), where they read sdemote and leave
-            const int top = 1 + RD * ((i - 1) / RD + 1);
-            for (int k = i + 1; k < top && k <= ni; k++) __syncthreads();
-            break;
-        }
+        if (leave) dem_i = i;  // (the evaluators leave after this interval's barrier too)
     }
 #ifdef FMRX_AB_PROF
     if (t == 0) {
@@ -1577,9 +1609,8 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
     auto sE = [&](int sl, int J, int l) -> float& { return reinterpret_cast<float*>(&sR[sl][J >> 1][l])[2 * (J & 1) + 1]; };
     __shared__ uint32_t sbase[4][NI];
     __shared__ int srow[4][NI];
-    __shared__ float2 sst[4];
+    __shared__ float4 sst[4];  // (integ, phase, the verdict "redone exactly" as int bits, -)
     __shared__ int sexact[4];
-    __shared__ int sdemote;  // the interval after which the chain left (pll_demote), or 0
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
     const int s = blockIdx.x;  // grid = n_streams
     const float* x = io + (size_t)s * stride;
@@ -1596,7 +1627,7 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
         return step * (double)(float)fmin(t0d + (double)(j + 1), (double)kPllTrigStick);
     };
     const int nb = n / NI;
-    const int ni = nb > 0 ? nb - 1 : 0;  // intervals after interval 0 (exact)
+    const int ni = nb;  // intervals 1 .. nb from the range's first step (the first predicted too)
     // test hook: a forced miss on interval 1 + (inject + s) % ni (counted as resumed)
     const int inj = inject >= 0 && ni > 0 ? 1 + (inject + s) % ni : -1;
     auto exact = [&](PllState& q, PllCtx& c, long long j0, long long j1) {
@@ -1622,7 +1653,7 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
         }
         return;
     }
-    auto j0 = [](int k) { return NI * k; };  // interval k's first step
+    auto j0 = [](int k) { return NI * (k - 1); };  // interval k's first step (k >= 1)
     // the rows' constant slots, once: T slot NC + 1 = +inf (never counted), E slots 0 and NC + 1 NaN
     for (int q = threadIdx.x; q < 4 * NI; q += 64 * (1 + NW)) {
         sT(q / NI, q % NI, NC + 1) = __builtin_inff();
@@ -1669,6 +1700,11 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
                 if (kc == 0) sbase[sl][J] = cb - (uint32_t)HC - 1u;
             }
         };
+        // test hook pll_pipe_miss = -m (m >= 2): every interval from m - 1 on misses -- step 0's E row
+        // NaN (the lanes of wave 1 that wrote it in put)
+        auto hook_poison = [&](int k) {
+            if (miss <= -2 && k >= -miss - 1 && w == 1 && t < NC) sE(k & 3, 0, t + 1) = __builtin_nanf("");
+        };
         // wave 1: interval k's trigArgs, bits(c_base) - 1 + the chain's count (the chain stored a
         // redone interval itself)
         auto store = [&](int k) {
@@ -1683,34 +1719,33 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
         };
 #pragma unroll
         for (int u = 0; u < RD; u++) ld(1 + u, vq[(1 + u) % RD]);
-        put(1, p.phase, vq[1 % RD]);  // interval 1 from the phase at interval 0's start
+        put(1, p.phase, vq[1 % RD]);  // interval 1 from the start phase (its own start)
+        hook_poison(1);
         ld(1 + RD, vq[1 % RD]);
         __syncthreads();  // (prologue)
         unsigned long long ev_body = 0, ev_wait = 0;
-        // the chain demoted the stream (pll_demote) after redoing interval i - 1 itself: it runs the
-        // rest of the range alone, no barrier is reached any more
-        bool demoted = false;
-        for (int i0 = 1; i0 <= ni && !demoted; i0 += RD) {
+        // pll_demote is the chain's (its verdicts are at hand there, a few scalar ops an interval):
+        // when it leaves after interval i - 1 it says so in that interval's state word (w), and the
+        // evaluators store that interval's trigArgs and leave too, without another barrier
+        bool left = false;
+        for (int i0 = 1; i0 <= ni && !left; i0 += RD) {
             unroll_ic(
                 [&](auto uc) {
                     constexpr int u = decltype(uc)::value;
                     constexpr int sl = (2 + u) % RD;  // slot of interval i + 1
                     const int i = i0 + u;
-                    if (i <= ni && !demoted) {
-                        // once a group of RD intervals: has the chain left (pll_demote) after an
-                        // interval before this one?  sdemote names it; the chain takes the barriers
-                        // of the intervals in between (those evaluations and stores are wasted and
-                        // the rest of the range is pll_demoted_kernel's, which rewrites them)
-                        if (u == 0 && !kAbNoDemote) {
-                            const int dm = __builtin_amdgcn_readfirstlane(sdemote);
-                            if (dm != 0 && dm < i) {
-                                demoted = true;
-                                return;
-                            }
-                        }
+                    if (i <= ni && !left) {
                         const unsigned long long p0 = PROF_T();
+                        // the chain's state at interval i's start (and whether it left there)
+                        const float4 rs = sst[(i - 1) & 3];
+                        if (!kAbNoDemote && __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, rs.w)) != 0) {
+                            store(i - 1);
+                            left = true;
+                            return;
+                        }
                         if (i + 1 <= ni) {
-                            put(i + 1, sst[(i - 1) & 3].y, vq[sl]);  // from the phase at interval i's start
+                            put(i + 1, rs.y, vq[sl]);  // from the phase at interval i's start
+                            hook_poison(i + 1);
                             ld(i + 1 + RD, vq[sl]);
                         }
                         store(i - 1);
@@ -1722,7 +1757,7 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
                 },
                 std::make_integer_sequence<int, RD>{});
         }
-        if (!demoted) store(ni);
+        if (!left) store(ni);
 #ifdef FMRX_AB_PROF
         if (t == 0 && w == 1) {
             atomicAdd(&g_cnt_prof[2], ev_body);
@@ -1735,9 +1770,8 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
     }
 
     // ---- the chain
-    PllCtx ctx{};
-    ctx.valid = false;
-    exact(p, ctx, 0, NI);  // interval 0 on the exact path
+    // interval 1 starts at the range's first step, predicted from the start phase like every other
+    // (until round 6 a whole interval ran first on the exact path, at ~400 ns a step)
     float integ = p.integ, phase = p.phase;
     // the carry: the E row of the previous trigArg and its count (SGPR); after an exact stretch
     // that trigArg's exact e in every lane
@@ -1747,21 +1781,30 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
         cE = exact_e(a, x[min(j0(k), n - 1)]);
         cC = 1;
     };
-    carry_exact((float)ctx.x, 1);
+    cE = exact_e_fb(p.fbI, p.fbQ, x[0]);  // step 0's e from the state's feedback (every lane)
     if (t == 0) {
-        sst[0] = make_float2(integ, phase);
+        // the start state; its verdict (z) reads as a hit (no prediction pll_demote counts), and
+        // no i >= 2 test in the evaluators' loop (LLVM peels a whole unrolled iteration for one)
+        sst[0] = make_float4(integ, phase, 0.0f, 0.0f);
         sexact[0] = 1;
-        sdemote = 0;
     }
     __syncthreads();  // (prologue)
-    uint32_t hist = 0;  // the last 32 intervals' verdicts (pll_demote)
-    int dem_i = 0;      // the interval after which the chain left (pll_demote), or 0
+    // pll_demote: the chain's verdicts of its last 32 intervals (SGPR bits); past kPllDemoteMisses
+    // misses it leaves after the interval (dem_i) and the demoted kernel runs the rest
+    int dem_i = 0;
+    uint32_t hist = 0;
     unsigned long long n_redo = 0, n_inj = 0, ch_body = 0, ch_wait = 0;
     const int ls = t < NP ? t : NP - 1;  // this lane's row slot (lanes past the row read its last)
-    for (int i = 1; i <= ni; i++) {
+    uint32_t prev_bad = 0;  // the last interval's verdict (SGPR)
+    for (int i = 1; i <= ni && dem_i == 0; i++) {
         const unsigned long long p0 = PROF_T();
         const int is = i & 3;
         const float integ0 = integ, phase0 = phase;
+        // the verdicts up to interval i - 1 decide whether the chain leaves after this one: scalar
+        // work at the interval's start, off the chain's path (at its end it delayed the barrier)
+        hist = (hist << 1) | prev_bad;
+        const bool leave = !kAbNoDemote && i < ni && n >= kPllDemoteMinIntervals * NI &&
+                           __builtin_popcount(hist) >= kPllDemoteMisses;
         int row[NRW] = {};
         unroll_ic(
             [&](auto hc) {
@@ -1800,15 +1843,18 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
         // start state in pll_batch_fast's range; test hooks force misses
         const float ce = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cE), cC));
         const bool bad = !(phase == phase) || !(ce == ce) ||
-                         !(fabsf(phase0) < kPllMaxPhase && fabsf(integ0) < kPllMaxInteg) || pll_hook_miss(i, miss, ni) ||
+                         !(fabsf(phase0) < kPllMaxPhase && fabsf(integ0) < kPllMaxInteg) || i == min(miss, ni) ||
                          i == inj;
         if (bad) {  // uniform: redo the interval exactly from its start (the chain stores it)
             n_redo++;
             n_inj += i == inj ? 1 : 0;
-            const float a = (float)(pr_at(j0(i) - 1) + (double)phase0);  // the trigArg before it
-            PllState q;
+            PllState q = p;  // interval 1: the range's start state as given
             PllCtx c{};
-            pll_state_at(q, c, integ0, phase0, trig0, (long long)j0(i), a, DeviceLib{});
+            c.valid = false;
+            if (i > 1) {
+                const float a = (float)(pr_at(j0(i) - 1) + (double)phase0);  // the trigArg before it
+                pll_state_at(q, c, integ0, phase0, trig0, (long long)j0(i), a, DeviceLib{});
+            }
             exact(q, c, j0(i), j0(i) + NI);
             integ = q.integ;
             phase = q.phase;
@@ -1817,27 +1863,14 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
 #pragma unroll
         for (int r = 0; r < NRW; r++)
             if (t + 64 * r < NI) srow[is][t + 64 * r] = row[r];
-        // demoted right after a redo (pll_idx_kernel's rule)
-        // (bad is uniform but VGPR-derived: taken through an SGPR, so hist, the demotion and the
-        // loop exit stay scalar -- a divergent exit would turn the whole interval loop into a
-        // masked one, measured ~4 ns a step slower on the index forms)
-        const bool bad_u = __builtin_amdgcn_readfirstlane((int)bad) != 0;
-        const bool dem = !kAbNoDemote && pll_demote(hist, bad_u) && bad_u && i < ni;
-        sst[is] = make_float2(integ, phase);
+        prev_bad = (uint32_t)__builtin_amdgcn_readfirstlane(bad ? 1 : 0);  // (scalar: no divergent loop)
+        sst[is] = make_float4(integ, phase, __builtin_bit_cast(float, bad ? 1 : 0), __builtin_bit_cast(float, leave ? 1 : 0));
         sexact[is] = bad ? 1 : 0;
-        if (dem) sdemote = i;
         const unsigned long long p1 = PROF_T();
         __syncthreads();
         ch_body += p1 - p0;
         ch_wait += PROF_T() - p1;
-        if (dem) {
-            dem_i = i;
-            // the evaluators' barriers up to the top of their next group of RD intervals (from
-            // interval 1), where they read sdemote and leave
-            const int top = 1 + RD * ((i - 1) / RD + 1);
-            for (int k = i + 1; k < top && k <= ni; k++) __syncthreads();
-            break;
-        }
+        if (leave) dem_i = i;  // (the evaluators leave after this interval's barrier too)
     }
 #ifdef FMRX_AB_PROF
     if (t == 0) {
@@ -1957,7 +1990,10 @@ void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_
     reg_pred_prof();
 #endif
     if (n <= 0) return;
-    if (form == 23)
+    if (form == 24)  // the short-call form: any trigOffset from 2^20, 16-step intervals
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 1, FMRX_PIPE_RD, 5, false, true>), dim3(n_streams), dim3(192), 0, s,
+                           io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
+    else if (form == 23)
         hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, FMRX_STICK_BPI, FMRX_PIPE_RD, 3, true>), dim3(n_streams), dim3(192), 0, s, io, n,
                            n_streams, stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
     else if (form == 22)
@@ -2045,6 +2081,19 @@ static int cnt_launch(hipStream_t s, const float* io, int n, int n_streams, size
 #ifndef FMRX_CNT_NW
 #define FMRX_CNT_NW 4  // evaluator waves of the [2^19, 2^21) count forms
 #endif
+#ifndef FMRX_CNT17_NI
+#define FMRX_CNT17_NI 16  // steps an interval of the [2^17, 2^19) count forms (off by default)
+#endif
+#ifndef FMRX_CNT17_NW
+#define FMRX_CNT17_NW 4  // their evaluator waves
+#endif
+int pll_form_interval(int form, bool cnt) {
+    if (cnt) return form <= 18 ? FMRX_CNT17_NI : form == 19 ? FMRX_CNT19_NI : form == 20 ? FMRX_CNT20_NI : 64;
+    if (form < 20) return 16;  // the index runner
+    return form == 20 || form == 24 ? kPllBatch : form == 21 ? kPllBatch * FMRX_PIPE21_BPI
+         : form == 22 ? kPllBatch * FMRX_PIPE22_BPI : kPllBatch * FMRX_STICK_BPI;
+}
+
 int launch_pll_cnt(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step, float norm_bw,
                    float* st, float* out, size_t ostride, int inject, int miss, int form, unsigned long long* stats,
                    unsigned* redos) {
@@ -2054,10 +2103,10 @@ int launch_pll_cnt(hipStream_t s, const float* io, int n, int n_streams, size_t 
     if (n <= 0) return 0;
     switch (form) {
         case 17:
-            return cnt_launch<16, 31, 4>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
+            return cnt_launch<FMRX_CNT17_NI, 31, FMRX_CNT17_NW>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
                                          131072.0f, 262143.0f, stats, redos);
         case 18:
-            return cnt_launch<16, 31, 4>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
+            return cnt_launch<FMRX_CNT17_NI, 31, FMRX_CNT17_NW>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,
                                          262144.0f, 524287.0f, stats, redos);
         case 19:
             return cnt_launch<FMRX_CNT19_NI, 15, FMRX_CNT_NW>(s, io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss,

@@ -72,9 +72,31 @@ __global__ void __launch_bounds__(kBpThreads) bpf_pair_tile_kernel(StereoLaunch 
     const long long j0 = (long long)blockIdx.x * kBpTile;
     const float* x = L.demod + (size_t)s * L.demod_stride + L.hist + j0 - (BT - 1);
     const long long avail = (long long)L.n_if - j0 + (BT - 1);  // samples of this stream from x on
-    for (int i = tid; i < kBpTile + BT - 1; i += kBpThreads) {
-        const float v = i < avail ? x[i] : 0.0f;
-        xs2[i] = make_float2(v, v);
+    if (L.src) {  // the new samples from L.src (this tile's own ones also stored behind the history)
+        // every load issued before any store (src may be host memory: one round trip, not one per
+        // pass; src and demod could alias as far as the compiler knows)
+        constexpr int kPass = (kBpTile + BT - 1 + kBpThreads - 1) / kBpThreads;
+        const float* src = L.src + (size_t)s * L.n_if + j0 - (BT - 1);
+        float* dst = const_cast<float*>(x);
+        float v[kPass];
+#pragma unroll
+        for (int r = 0; r < kPass; r++) {
+            const int i = tid + kBpThreads * r;
+            const long long g = j0 - (BT - 1) + i;  // call index of sample i (< 0: history)
+            v[r] = i < kBpTile + BT - 1 && i < avail ? (g < 0 ? x[i] : src[i]) : 0.0f;
+        }
+#pragma unroll
+        for (int r = 0; r < kPass; r++) {
+            const int i = tid + kBpThreads * r;
+            if (i >= kBpTile + BT - 1) break;
+            if (i >= BT - 1 && i < avail) dst[i] = v[r];
+            xs2[i] = make_float2(v[r], v[r]);
+        }
+    } else {
+        for (int i = tid; i < kBpTile + BT - 1; i += kBpThreads) {
+            const float v = i < avail ? x[i] : 0.0f;
+            xs2[i] = make_float2(v, v);
+        }
     }
     __syncthreads();
     float2v win[2 * WV];
@@ -785,11 +807,13 @@ __global__ void stereo_audio_kernel(AudioLaunch L, int b0) {
 // delay line reads it back from LDS.  Same arithmetic as stereo_audio_kernel.
 constexpr int kTileIf = 1024, kTileFrames = 256, kTileTaps = 64;
 
-__global__ void __launch_bounds__(128) stereo_audio_tile_kernel(AudioLaunch L, int b0) {
+// carry (the small kernel's last block): the state carry from this tile's LDS instead of
+// audio_state_carry's global re-reads -- MO holds the block's monos (mono_at's sums, same
+// order) and X[H + i].y its mixer samples.
+__device__ void audio_tile(const AudioLaunch& L, int s, int b, bool carry = false) {
     constexpr int kPer = kTileFrames / 128;    // frames per thread
     __shared__ float2 X[kTileTaps + kTileIf];  // X[H + j]: (mono input, stereo input) at IF index j
     __shared__ float C[kTileTaps], MO[kTileFrames];
-    const int s = blockIdx.y, b = b0 + (int)blockIdx.x;  // block b of the call
     const int ipb = L.if_per_block, fpb = L.frames_per_block, at = L.at, H = at - 1;
     const AudioView cur = view(L, s, b);
     for (int i = threadIdx.x; i < ipb; i += blockDim.x) X[H + i] = make_float2(cur.d[i], mixer_at(cur, i));
@@ -846,12 +870,19 @@ __global__ void __launch_bounds__(128) stereo_audio_tile_kernel(AudioLaunch L, i
         L.pcm[2 * o + 1] = quantize_s16(left);
         if (L.mono_out) L.mono_out[o] = MO[m];
     }
+    if (!carry) return;
+    __syncthreads();  // every read of the old mono_state / mix_tail happened above
+    const int i = threadIdx.x;
+    if (i < kMonoDelay) L.mono_state[(size_t)s * 8 + i] = MO[fpb - kMonoDelay + i];
+    if (i < kTail) L.mix_tail[(size_t)s * kTail + i] = X[H + ipb - kTail + i].y;
 }
 
-// Carry the audio state of the LAST block of this call into the next call.
-__global__ void stereo_state_kernel(AudioLaunch L) {
-    const int s = blockIdx.x;
-    const int i = threadIdx.x;
+__global__ void __launch_bounds__(128) stereo_audio_tile_kernel(AudioLaunch L, int b0) {
+    audio_tile(L, blockIdx.y, b0 + (int)blockIdx.x);  // block b of the call, stream blockIdx.y
+}
+
+// Carry the audio state of the LAST block of this call into the next call (thread i of stream s).
+__device__ void audio_state_carry(const AudioLaunch& L, int s, int i) {
     const int b = L.n_blocks - 1;
     const AudioView cur = view(L, s, b);
     const AudioView prv = b > 0 ? view(L, s, b - 1) : cur;
@@ -865,6 +896,36 @@ __global__ void stereo_state_kernel(AudioLaunch L) {
     if (i < kTail) L.mix_tail[(size_t)s * kTail + i] = mix;
 }
 
+__global__ void stereo_state_kernel(AudioLaunch L) { audio_state_carry(L, blockIdx.x, threadIdx.x); }
+
+// A few blocks a stream (the reference's per-block seam, fmrx_audio_block with one block): the
+// NCO (pll_nco_kernel's arithmetic, from the PLL's trigArgs), every block's audio in order
+// (audio_tile), the state carry (stereo_state_kernel) and the demod history for the next call
+// (the last kDemodHist samples to the front) in ONE launch, one workgroup a stream -- four
+// launches fewer than the parallel path, which costs each of them ~4-7 us at this size
+// (profiles/r06/seam: kernel trace of the seam).
+__global__ void __launch_bounds__(128) stereo_audio_small_kernel(AudioLaunch L, const float* args, size_t astride,
+                                                                 float nco_scale, float phase_adjust, float* pll_st,
+                                                                 int demod_hist) {
+    const int s = blockIdx.x;
+    const int nif = L.n_blocks * L.if_per_block;
+    float* nco = const_cast<float*>(L.nco) + (size_t)s * nif;
+    for (int i = threadIdx.x; i < nif; i += blockDim.x) {  // filter.cpp:170 (pll_nco_kernel)
+        const float a = args[(size_t)s * astride + i] * nco_scale + phase_adjust;
+        float sv, cv;
+        if (!fast_sincos_f(a, &sv, &cv)) cv = sincos_lib(a).y;
+        nco[i] = cv;
+        if (i == nif - 1) pll_st[8 * (size_t)s + 4] = cv;
+    }
+    __syncthreads();
+    for (int b = 0; b < L.n_blocks; b++) {
+        audio_tile(L, s, b, b == L.n_blocks - 1);  // the last block carries the state
+        __syncthreads();
+    }
+    float* d = const_cast<float*>(L.demod) + (size_t)s * L.demod_stride;
+    for (int i = threadIdx.x; i < demod_hist; i += blockDim.x) d[i] = d[nif + i];
+}
+
 inline int ok() { return hipGetLastError() == hipSuccess ? 0 : -2; }
 
 }  // namespace
@@ -875,7 +936,13 @@ int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s, bool ti
     BpTaps t{};
     for (int k = 0; k < L.bp_taps; k++) t.c[k] = make_float2(L.ch_c[k], L.ca_c[k]);
     const dim3 grid((L.n_if + 255) / 256, n_streams), block(256);
-    if (L.bp_taps == 51 && L.hist >= 50 && tiled)
+    const bool tile = L.bp_taps == 51 && L.hist >= 50 && tiled;
+    if (L.src && !tile &&  // the per-output kernels read the new samples from demod: copy them there
+        hipMemcpy2DAsync(const_cast<float*>(L.demod) + L.hist, L.demod_stride * sizeof(float), L.src,
+                         (size_t)L.n_if * sizeof(float), (size_t)L.n_if * sizeof(float), n_streams,
+                         hipMemcpyDefault, s) != hipSuccess)
+        return -1;
+    if (tile)
         hipLaunchKernelGGL(bpf_pair_tile_kernel<51>, dim3((L.n_if + kBpTile - 1) / kBpTile, n_streams), dim3(kBpThreads),
                            0, s, L, t);
     else if (L.bp_taps == 51)
@@ -1055,21 +1122,14 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     // 16-step five-candidate form, [2^21, 2^22) the 64-step one, from 2^22 (the stick included)
     // three candidates
     int idx_rc = 0;
-    for (size_t j = n_seg; pipe && j < (size_t)n;) {
-        const double t = std::min(hlo + (double)j, (double)kPllTrigStick);
-        // form 23 (the stuck trigOffset, 2^24): the three-candidate runner's stick form (pll_stick)
-        const bool stick = kn.stick != 0;
-        const int form = t < 262144.0 ? 17 : t < 524288.0 ? 18 : t < (double)kPllPipeMinLow ? 19
-                       : t < (double)kPllPipeMin5 ? 20 : t < (double)kPllPipeMin ? 21
-                       : (!stick || t < (double)kPllTrigStick) ? 22 : 23;
-        const double edge = form == 17 ? 262144.0 : form == 18 ? 524288.0 : form == 19 ? (double)kPllPipeMinLow
-                          : form == 20 ? (double)kPllPipeMin5 : form == 21 ? (double)kPllPipeMin
-                          : form == 22 && stick ? (double)kPllTrigStick : 0.0;
-        const size_t e = edge == 0.0 ? (size_t)n : std::min((size_t)(edge - hlo), (size_t)n);
-        const bool cnt = form < 22 && ((kn.cnt >> (form - 17)) & 1) && kPllIdxSimds * n_streams <= n_simd;
+    // a short call (the per-block seam: 640 steps a call) runs the 16-step forms only: a long
+    // form's first interval (the count forms) and its steps past the last whole interval (all
+    // forms) run on the exact path at ~400 ns a step -- up to 255 steps a call, every call
+    const bool short_call = (size_t)n < kPllShortCall;
+    auto run = [&](int form, bool cnt, size_t j, size_t e) {
         const int kind = cnt ? kStCnt17 + (form - 17)
                        : form == 17 ? kStIdx17 : form == 18 ? kStIdx18 : form == 19 ? kStIdx19
-                       : form == 20 ? kStPipe20 : form == 21 ? kStPipe21 : form == 22 ? kStPipe22 : kStStick;
+                       : form == 20 || form == 24 ? kStPipe20 : form == 21 ? kStPipe21 : form == 22 ? kStPipe22 : kStStick;
         timed(kind, (double)(e - j), [&] {
             if (cnt)
                 idx_rc |= launch_pll_cnt(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j,
@@ -1080,10 +1140,43 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
             else
                 launch_pll_pipe(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j, (size_t)n,
                                 inject, pipe_miss, form, spec_stats, hint.redos);
-            // the streams that launch demoted (an unlocked loop): the rest of its range
-            idx_rc |= launch_pll_demoted(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j,
-                                         (size_t)n, inject, spec_stats);
+            // the streams that launch demoted (an unlocked loop): the rest of its range -- queued
+            // exactly where the runner may demote (kPllDemoteMinIntervals, the same rule there)
+            if ((e - j) >= (size_t)kPllDemoteMinIntervals * (size_t)pll_form_interval(form, cnt))
+                idx_rc |= launch_pll_demoted(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j,
+                                             (size_t)n, inject, spec_stats);
         });
+    };
+    for (size_t j = n_seg; pipe && j < (size_t)n;) {
+        const double t = std::min(hlo + (double)j, (double)kPllTrigStick);
+        // form 23 (the stuck trigOffset, 2^24): the three-candidate runner's stick form (pll_stick)
+        const bool stick = kn.stick != 0;
+        const int form = t < 262144.0 ? 17 : t < 524288.0 ? 18 : t < (double)kPllPipeMinLow ? 19
+                       : t < (double)kPllPipeMin5 ? 20 : t < (double)kPllPipeMin ? 21
+                       : (!stick || t < (double)kPllTrigStick) ? 22 : 23;
+        const double edge = form == 17 ? 262144.0 : form == 18 ? 524288.0 : form == 19 ? (double)kPllPipeMinLow
+                          : form == 20 ? (double)kPllPipeMin5 : form == 21 ? (double)kPllPipeMin
+                          : form == 22 && stick ? (double)kPllTrigStick : 0.0;
+        size_t e = edge == 0.0 ? (size_t)n : std::min((size_t)(edge - hlo), (size_t)n);
+        const bool cnt = form < 22 && ((kn.cnt >> (form - 17)) & 1) && kPllIdxSimds * n_streams <= n_simd;
+        const size_t len = e - j, ni = (size_t)pll_form_interval(form, cnt);
+        // the 16-step forms (the index runner below 2^20, the wide three-wave form 24 from 2^20 to the
+        // end of a short call) for a short call and for a range of few long intervals
+        if (ni > 16 && (short_call || len < kPllShortIntervals * ni)) {
+            if (form >= 20 && short_call) e = (size_t)n;
+            run(form >= 20 ? 24 : form, false, j, e);
+            j = e;
+            continue;
+        }
+        // a long form: its whole intervals, then the tail on the 16-step form (when it is long enough
+        // for one: below, it runs exactly in the long launch)
+        size_t body = len;
+        if (ni > 16) {
+            body = len / ni * ni;
+            if (len - body < kPllShortTail) body = len;
+        }
+        run(form, cnt, j, j + body);
+        if (body < len) run(form >= 20 ? 24 : form, false, j + body, e);
         j = e;
     }
     // the NCO of every sample from its trigArg (filter.cpp:170), in parallel, over the input in place
@@ -1125,6 +1218,20 @@ int launch_stereo_audio_range(const AudioLaunch& L, int b0, int b1, bool last, i
         }
     }
     if (last) hipLaunchKernelGGL(stereo_state_kernel, dim3(n_streams), dim3(kTail), 0, s, L);
+    return ok();
+}
+
+const float* pll_trig_args(const double* side, int n, int n_streams) {
+    return reinterpret_cast<const float*>(side + 4 * pll_seg_len(n, n_streams) * (size_t)n_streams);
+}
+
+int launch_stereo_audio_small(const AudioLaunch& L, int n_streams, const float* args, size_t astride, float nco_scale,
+                              float phase_adjust, float* pll_st, int demod_hist, hipStream_t s) {
+    if (L.up != 1 || L.if_per_block > kTileIf || L.frames_per_block > kTileFrames || L.at > kTileTaps ||
+        L.if_per_block < kTail || L.n_blocks < 1 || demod_hist > L.n_blocks * L.if_per_block)
+        return -1;
+    hipLaunchKernelGGL(stereo_audio_small_kernel, dim3(n_streams), dim3(128), 0, s, L, args, astride, nco_scale,
+                       phase_adjust, pll_st, demod_hist);
     return ok();
 }
 

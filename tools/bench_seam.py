@@ -8,6 +8,7 @@ reference's threads hold them (INTEGRATION.md Option 1).
   two_threads  two contexts (rx_rf, rx_audio), the reference's thread split: thread A runs
                fmrx_rf_block and queues the demod block, thread B runs fmrx_audio_block on it
                (ctypes releases the GIL inside each call), blocks per second over the run
+  native       both legs again from C++ (bin/fmrx_seam, csrc/seam_bench.cpp)
   cli          the fmrx CLI (bin/fmrx 0 2) on the same stream from a file, at its default
                --batch 16 and at --batch 2048
 
@@ -16,7 +17,6 @@ Mode-0 stereo (the reference's product), synthetic stream 5.  Prints one JSON li
     python tools/bench_seam.py [--blocks 3000] [--cli-mib 256]
 """
 import argparse
-import ctypes as C
 import json
 import os
 import queue
@@ -55,7 +55,9 @@ def main():
     iq = fm.synth_host(5, geo.rf_fs, 0, nb * bb // 2)
     demod = np.zeros((nb, nif), np.float32)
     pcm = np.zeros((nb, npcm), np.int16)
-    ptr = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    # raw addresses (argtypes c_void_p take ints): no slice or ctypes object per call
+    iq_p, dm_p, pcm_p = iq.ctypes.data, demod.ctypes.data, pcm.ctypes.data
+    dm_b, pcm_b = demod.strides[0], pcm.strides[0]
     res = {"config": f"mode-0 stereo, one block = {bb} B = {budget * 1e3:.3f} ms of signal, {args.blocks} timed "
                      f"blocks after {args.warmup} warm-up blocks, host buffers (fmrx_rf_block / fmrx_audio_block)",
            "block_budget_ms": round(budget * 1e3, 4)}
@@ -65,9 +67,9 @@ def main():
         t_rf, t_au, t_blk = [], [], []
         for b in range(nb):
             t0 = time.perf_counter()
-            rc = L.fmrx_rf_block(rx.h, ptr(iq[b * bb:(b + 1) * bb]), 1, ptr(demod[b]))
+            rc = L.fmrx_rf_block(rx.h, iq_p + b * bb, 1, dm_p + b * dm_b)
             t1 = time.perf_counter()
-            rc |= L.fmrx_audio_block(rx.h, ptr(demod[b]), 1, ptr(pcm[b]))
+            rc |= L.fmrx_audio_block(rx.h, dm_p + b * dm_b, 1, pcm_p + b * pcm_b)
             t2 = time.perf_counter()
             assert rc == 0, fm.lib().fmrx_last_error()
             if b >= args.warmup:
@@ -81,6 +83,7 @@ def main():
 
     # two contexts on two threads, a queue between them (project.cpp's producer / consumer)
     pcm2 = np.zeros_like(pcm)
+    pcm2_p = pcm2.ctypes.data
     with fm.Receiver(0, fm.STEREO) as rx_rf, fm.Receiver(0, fm.STEREO) as rx_au:
         q = queue.Queue(maxsize=16)  # project.cpp QUEUE_CAPACITY-like bound
         err = []
@@ -90,14 +93,14 @@ def main():
             for b in range(nb):
                 if b == args.warmup:
                     t_start[0] = time.perf_counter()
-                if L.fmrx_rf_block(rx_rf.h, ptr(iq[b * bb:(b + 1) * bb]), 1, ptr(demod[b])):
+                if L.fmrx_rf_block(rx_rf.h, iq_p + b * bb, 1, dm_p + b * dm_b):
                     err.append("rf")
                 q.put(b)
             q.put(None)
 
         def au():
             while (b := q.get()) is not None:
-                if L.fmrx_audio_block(rx_au.h, ptr(demod[b]), 1, ptr(pcm2[b])):
+                if L.fmrx_audio_block(rx_au.h, dm_p + b * dm_b, 1, pcm2_p + b * pcm_b):
                     err.append("audio")
 
         ta, tb = threading.Thread(target=rf), threading.Thread(target=au)
@@ -112,6 +115,15 @@ def main():
     res["two_threads"] = {"blocks_per_s": round(args.blocks / span, 1), "x_realtime": round(args.blocks * budget / span, 2),
                           "seconds": round(span, 4), "pcm_equals_serial": bool(np.array_equal(pcm2, serial_pcm)),
                           "note": "wall span of the timed blocks; every stage call returns with its output on the host"}
+
+    # the same two legs from C++ (bin/fmrx_seam: project.cpp's own call pattern, no interpreter
+    # between the calls), on the same stream
+    seam_exe = os.path.join(os.path.dirname(fm.LIB_PATH), "bin", "fmrx_seam")
+    r = subprocess.run([seam_exe, "--blocks", str(args.blocks), "--warmup", str(args.warmup)],
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
+    if r.returncode != 0:
+        raise SystemExit(f"{seam_exe} failed ({r.returncode}): {r.stderr.decode()[-400:]}")
+    res["native"] = json.loads(r.stdout.decode())
 
     # the CLI on the same synthetic stream from a file, default batch and the large batch
     exe = os.path.join(os.path.dirname(fm.LIB_PATH), "bin", "fmrx")
