@@ -38,7 +38,10 @@ namespace {
 constexpr int kDemNB = kPllBatch;       // steps a batch (verified as one)
 constexpr int kDemSB = 16;              // batches a sub-segment
 constexpr int kDemL = kDemNB * kDemSB;  // steps a sub-segment
-constexpr int kDemW = 4;                // waves: the chain and three checkers
+#ifndef FMRX_DEM_W
+#define FMRX_DEM_W 4
+#endif
+constexpr int kDemW = FMRX_DEM_W;       // waves: the chain and the checkers
 
 __device__ inline double dem_iv(float v) {  // pll_check_kernel's 1/v (pll_side's NaN outside the range)
     const double vd = (double)v;
@@ -132,14 +135,19 @@ __device__ __noinline__ bool dem_verify(const float* x, int J, float integ, floa
     return same && __float_as_uint(p.integ) == __float_as_uint(ei) && __float_as_uint(p.phase) == __float_as_uint(ep);
 }
 
-__global__ void __launch_bounds__(64 * kDemW) __attribute__((amdgpu_waves_per_eu(1, 1)))
+#ifndef FMRX_DEM_WPE
+#define FMRX_DEM_WPE 1  // waves a SIMD the register budget allows (A/B: 2 = 256 VGPRs, co-resident with stage kernels)
+#endif
+__global__ void __launch_bounds__(64 * kDemW) __attribute__((amdgpu_waves_per_eu(FMRX_DEM_WPE, FMRX_DEM_WPE)))
 pll_demoted_kernel(const float* io, int n, size_t stride, double step, float norm_bw, float* st, float* out_base,
                    size_t ostride, int inject, unsigned long long* stats) {
     constexpr int NB = kDemNB, SB = kDemSB, L = kDemL;
     const int s = blockIdx.x;
-    // the first step the runner launch before left to this kernel (state slot 6, int bits; 0 none)
-    const int j0 = __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, st[8 * (size_t)s + 6]));
-    if (j0 <= 0 || j0 >= n) return;  // not demoted (uniform: no barrier reached)
+    // the steps the call's runner launches left to this kernel, up to the end of its range (state
+    // slot 6, int bits; 0 none): launch_pll queues it once, after them, over the call's runner ranges
+    const int rem = __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, st[8 * (size_t)s + 6]));
+    if (rem <= 0 || rem >= n) return;  // not demoted (uniform: no barrier reached)
+    const int j0 = n - rem;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
     const float* x = io + (size_t)s * stride + j0;  // the demoted rest of the range: steps [0, m)
     float* out = out_base + (size_t)s * ostride + j0;

@@ -80,6 +80,11 @@ constexpr int kPllBatch = 16;
 // instead of paying a failed interval plus its redo each time.  Locked streams miss <= ~1 % of
 // intervals (profiles/r05 redos); unlocked ones 75-100 % (profiles/r06/unlocked.json).
 constexpr int kPllDemoteMisses = 24;
+// the index forms ([2^17, 2^20), 16-step intervals, the tightest candidate windows) want 28: there
+// locked streams miss in bursts -- at 24, 20 of configs[4]'s 256 synth streams demoted and their
+// demoted steps ran after the runner launch (0.4206 vs 0.4098 s at 28, none demoted at 28 or 32;
+// profiles/r06/demote_probe/); the unlocked streams still demote within their first ~30 intervals
+constexpr int kPllDemoteMissesIdx = 28;
 // only a runner launch of at least this many intervals demotes (launch_pll queues the demoted kernel
 // after exactly those: a shorter range cannot pay for it, e.g. the per-block seam's 640 steps)
 constexpr int kPllDemoteMinIntervals = 64;

@@ -655,6 +655,15 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     // branch and loop after it stay scalar
     auto uni = [](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v))); };
     PllState p{uni(S[0]), uni(S[1]), uni(S[2]), uni(S[3]), uni(S[5])};
+    // demoted by an earlier runner launch of this call (pll_demote; state slot 6: the steps it left
+    // to pll_demoted_kernel, int bits): this range is theirs too -- add it and leave (uniform)
+    if (const int rem = __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, S[6])); rem > 0) {
+        if (threadIdx.x == 0) {
+            S[6] = __builtin_bit_cast(float, rem + n);
+            if (redos) atomicAdd(&redos[kPllRedoSlots * (size_t)s + 4 + pll_redo_range(p.trig)], (unsigned)n);
+        }
+        return;
+    }
     // the variant's domain (uniform over the group): NC = 3 from 2^22; NC = 5 with 64-step
     // intervals in [2^21, 2^22), with 16-step ones in [2^20, 2^21)
     static_assert(!WIDE || (NC == 5 && BPI == 1 && !STK), "the wide form is the 16-step five-candidate one");
@@ -1169,7 +1178,7 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
     if (t == 0) {
         S[0] = q.integ; S[1] = q.phase; S[2] = q.fbI; S[3] = q.fbQ; S[5] = q.trig;
-        S[6] = __builtin_bit_cast(float, demoted ? (int)jd : 0);  // pll_demoted_kernel's first step, or 0
+        S[6] = __builtin_bit_cast(float, demoted ? (int)(n - jd) : 0);  // the steps left to pll_demoted_kernel, or 0
         // fmrx_debug_pll_stats: batches run; "resumed" only for the inject hook's forced redos
         // (the runner is exact by construction: its own redos of missed intervals are internal)
         if (stats) {
@@ -1266,6 +1275,15 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
     const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
     auto uni = [](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v))); };
     PllState p{uni(S[0]), uni(S[1]), uni(S[2]), uni(S[3]), uni(S[5])};
+    // demoted by an earlier runner launch of this call (pll_demote; state slot 6: the steps it left
+    // to pll_demoted_kernel, int bits): this range is theirs too -- add it and leave (uniform)
+    if (const int rem = __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, S[6])); rem > 0) {
+        if (threadIdx.x == 0) {
+            S[6] = __builtin_bit_cast(float, rem + n);
+            if (redos) atomicAdd(&redos[kPllRedoSlots * (size_t)s + 4 + pll_redo_range(p.trig)], (unsigned)n);
+        }
+        return;
+    }
     const bool in_domain = pll_pipe_stream(p.trig, step, lo, hi);
     const float trig0 = p.trig;
     const double t0d = (double)trig0;
@@ -1441,7 +1459,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         // work at the interval's start, off the chain's path (at its end it delayed the barrier)
         hist = (hist << 1) | prev_bad;
         const bool leave = !kAbNoDemote && i < ni && n >= kPllDemoteMinIntervals * NI &&
-                           __builtin_popcount(hist) >= kPllDemoteMisses;
+                           __builtin_popcount(hist) >= kPllDemoteMissesIdx;
         // the interval's data before its steps (NI 16-byte broadcasts, NR row reads)
         float4 D[NI];
         float E[NR];
@@ -1524,7 +1542,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
     if (n_dem == 0) exact(q, c, jf, n);
     if (t == 0) {
         S[0] = q.integ; S[1] = q.phase; S[2] = q.fbI; S[3] = q.fbQ; S[5] = q.trig;
-        S[6] = __builtin_bit_cast(float, n_dem ? (int)jf : 0);  // pll_demoted_kernel's first step, or 0
+        S[6] = __builtin_bit_cast(float, n_dem ? (int)(n - jf) : 0);  // the steps left to pll_demoted_kernel, or 0
         if (stats) {
             atomicAdd(stats, n_inj);  // "resumed": the inject hook's forced redos only
             atomicAdd(stats + 1, (unsigned long long)nb);
@@ -1620,6 +1638,15 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
     const float Ki = (norm_bw * norm_bw) * static_cast<float>(3.555);
     auto uni = [](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v))); };
     PllState p{uni(S[0]), uni(S[1]), uni(S[2]), uni(S[3]), uni(S[5])};
+    // demoted by an earlier runner launch of this call (pll_demote; state slot 6: the steps it left
+    // to pll_demoted_kernel, int bits): this range is theirs too -- add it and leave (uniform)
+    if (const int rem = __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, S[6])); rem > 0) {
+        if (threadIdx.x == 0) {
+            S[6] = __builtin_bit_cast(float, rem + n);
+            if (redos) atomicAdd(&redos[kPllRedoSlots * (size_t)s + 4 + pll_redo_range(p.trig)], (unsigned)n);
+        }
+        return;
+    }
     const bool in_domain = pll_pipe_stream(p.trig, step, lo, hi);
     const float trig0 = p.trig;
     const double t0d = (double)trig0;
@@ -1893,7 +1920,7 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
     if (n_dem == 0) exact(q, c, jf, n);
     if (t == 0) {
         S[0] = q.integ; S[1] = q.phase; S[2] = q.fbI; S[3] = q.fbQ; S[5] = q.trig;
-        S[6] = __builtin_bit_cast(float, n_dem ? (int)jf : 0);  // pll_demoted_kernel's first step, or 0
+        S[6] = __builtin_bit_cast(float, n_dem ? (int)(n - jf) : 0);  // the steps left to pll_demoted_kernel, or 0
         if (stats) {  // in 16-step batches, as every runner counts
             atomicAdd(stats, n_inj * (NI / kPllBatch));  // "resumed": the inject hook's forced redos only
             atomicAdd(stats + 1, (unsigned long long)(n / kPllBatch));

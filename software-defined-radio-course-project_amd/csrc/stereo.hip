@@ -60,7 +60,7 @@ __global__ void __launch_bounds__(256) bpf_pair_kernel(StereoLaunch L, BpTaps t)
 // ms per call at 1,024 streams x 10 s.  Measured and dropped: workgroups walking 8 tiles with
 // the next tile's loads in flight, and 8 outputs a thread (the taps then spill from SGPRs).
 constexpr int kBpR = 4, kBpThreads = 256, kBpTile = kBpR * kBpThreads;  // (the pin below names 4)
-template <int BT>
+template <int BT, bool SRC>
 __global__ void __launch_bounds__(kBpThreads) bpf_pair_tile_kernel(StereoLaunch L, BpTaps t) {
     constexpr int W = kBpR + BT - 1;  // a thread's window: samples 4 tid .. 4 tid + W - 1 of the tile
     constexpr int WV = (W + 1) / 2;   // float4 reads (two duplicated samples each)
@@ -72,7 +72,7 @@ __global__ void __launch_bounds__(kBpThreads) bpf_pair_tile_kernel(StereoLaunch 
     const long long j0 = (long long)blockIdx.x * kBpTile;
     const float* x = L.demod + (size_t)s * L.demod_stride + L.hist + j0 - (BT - 1);
     const long long avail = (long long)L.n_if - j0 + (BT - 1);  // samples of this stream from x on
-    if (L.src) {  // the new samples from L.src (this tile's own ones also stored behind the history)
+    if constexpr (SRC) {  // the new samples from L.src (this tile's own ones also stored behind the history)
         // every load issued before any store (src may be host memory: one round trip, not one per
         // pass; src and demod could alias as far as the compiler knows)
         constexpr int kPass = (kBpTile + BT - 1 + kBpThreads - 1) / kBpThreads;
@@ -942,9 +942,12 @@ int launch_bpf_pair(const StereoLaunch& L, int n_streams, hipStream_t s, bool ti
                          (size_t)L.n_if * sizeof(float), (size_t)L.n_if * sizeof(float), n_streams,
                          hipMemcpyDefault, s) != hipSuccess)
         return -1;
-    if (tile)
-        hipLaunchKernelGGL(bpf_pair_tile_kernel<51>, dim3((L.n_if + kBpTile - 1) / kBpTile, n_streams), dim3(kBpThreads),
-                           0, s, L, t);
+    if (tile && L.src)
+        hipLaunchKernelGGL((bpf_pair_tile_kernel<51, true>), dim3((L.n_if + kBpTile - 1) / kBpTile, n_streams),
+                           dim3(kBpThreads), 0, s, L, t);
+    else if (tile)
+        hipLaunchKernelGGL((bpf_pair_tile_kernel<51, false>), dim3((L.n_if + kBpTile - 1) / kBpTile, n_streams),
+                           dim3(kBpThreads), 0, s, L, t);
     else if (L.bp_taps == 51)
         hipLaunchKernelGGL(bpf_pair_kernel<51>, grid, block, 0, s, L, t);
     else
@@ -1126,6 +1129,10 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     // form's first interval (the count forms) and its steps past the last whole interval (all
     // forms) run on the exact path at ~400 ns a step -- up to 255 steps a call, every call
     const bool short_call = (size_t)n < kPllShortCall;
+    // pll_demoted_kernel, ONCE a call after its runner launches (a demoted stream's later launches
+    // only add their steps to its hand-off): each launch of it waits for whole CUs (448 VGPRs a
+    // wave), so one per runner range stalled configs[4]'s pipeline ~11 ms (profiles/r06/demote_probe/)
+    size_t dem_from = (size_t)n;
     auto run = [&](int form, bool cnt, size_t j, size_t e) {
         const int kind = cnt ? kStCnt17 + (form - 17)
                        : form == 17 ? kStIdx17 : form == 18 ? kStIdx18 : form == 19 ? kStIdx19
@@ -1140,11 +1147,10 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
             else
                 launch_pll_pipe(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j, (size_t)n,
                                 inject, pipe_miss, form, spec_stats, hint.redos);
-            // the streams that launch demoted (an unlocked loop): the rest of its range -- queued
-            // exactly where the runner may demote (kPllDemoteMinIntervals, the same rule there)
+            // a launch that may demote a stream (kPllDemoteMinIntervals, the runner's own rule): the
+            // demoted kernel follows the call's last runner launch, from the first such launch on
             if ((e - j) >= (size_t)kPllDemoteMinIntervals * (size_t)pll_form_interval(form, cnt))
-                idx_rc |= launch_pll_demoted(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j,
-                                             (size_t)n, inject, spec_stats);
+                dem_from = std::min(dem_from, j);
         });
     };
     for (size_t j = n_seg; pipe && j < (size_t)n;) {
@@ -1171,7 +1177,11 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         // a long form: its whole intervals, then the tail on the 16-step form (when it is long enough
         // for one: below, it runs exactly in the long launch)
         size_t body = len;
+#ifdef FMRX_AB_NO_TAIL_SPLIT  // A/B: the long form's tail on its own exact path
+        if (false) {
+#else
         if (ni > 16) {
+#endif
             body = len / ni * ni;
             if (len - body < kPllShortTail) body = len;
         }
@@ -1179,6 +1189,13 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         if (body < len) run(form >= 20 ? 24 : form, false, j + body, e);
         j = e;
     }
+#ifndef FMRX_AB_NO_DEMOTED_LAUNCH  // A/B timing only (a demoted stream's range would stay unrun)
+    if (dem_from < (size_t)n)
+        timed(kStTail, 0.0, [&] {
+            idx_rc |= launch_pll_demoted(s, io + dem_from, (int)((size_t)n - dem_from), n_streams, stride, step, norm_bw,
+                                         st, args + dem_from, (size_t)n, inject, spec_stats);
+        });
+#endif
     // the NCO of every sample from its trigArg (filter.cpp:170), in parallel, over the input in place
     if (nco)
         timed(kStNco, 0.0, [&] {
