@@ -668,8 +668,10 @@ int run_stereo_pipelined_body(fmrx_ctx* c, const uint8_t* d_iq, size_t n_blocks,
     auto side_of = [&](int k) { return (k & 1) ? c->d_pll_side2.p : c->d_pll_side.p; };
     auto pll = [&](size_t off, size_t m, double* side, bool nco) -> int {
         if (m == 0) return 0;
+        PllHint h = c->hint(c->pll_trig);
+        h.demote_once = true;  // one demoted-kernel launch a chunk (beside the stage kernels)
         if (launch_pll(c->d_carrier.p + off, (int)m, ns, n_if, 19000.0f, (float)c->geo.if_fs, 2.0f, 0.0f, 0.01f,
-                       c->d_pll.p, side, c->stream, c->hint(c->pll_trig), c->pll_stats, nco)) {
+                       c->d_pll.p, side, c->stream, h, c->pll_stats, nco)) {
             c->pll_trig.known = false;
             return fail(FMRX_EHIP, "PLL launch failed");
         }
@@ -1144,6 +1146,10 @@ int state_io(fmrx_ctx* c, uint8_t* buf, size_t bytes, bool put) {
         b.p += w * ns;
     }
     if ((rc = b.io(c, c->d_pll.p, ns * sizeof(float) * 8))) return rc;
+    // (slots 6-7 of each stream's PLL state are the runners' hand-off within a call, 0 between
+    // calls: a blob's values there are not trusted)
+    if (put)
+        HIPCHK(hipMemset2DAsync(c->d_pll.p + 6, 8 * sizeof(float), 0, 2 * sizeof(float), ns, c->stream));
     if ((rc = b.io(c, c->d_mix_tail.p, ns * sizeof(float) * kMixTail))) return rc;
     if ((rc = b.io(c, c->d_mono_state.p, ns * sizeof(float) * 8))) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1520,6 +1526,8 @@ int fmrx_pll(fmrx_ctx* c, float* d_io, int n, float freq, float fs, float nco_sc
     rc = c->d_scratch.ensure(8);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(c->d_scratch.p, d_st, 6 * sizeof(float), hipMemcpyDeviceToDevice, c->stream));
+    // slots 6-7 are the runners' (6: the demoted hand-off, read by every runner launch): zero
+    HIPCHK(hipMemsetAsync(c->d_scratch.p + 6, 0, 2 * sizeof(float), c->stream));
     if ((rc = c->d_pll_side.ensure(pll_side_doubles(n, 1)))) return rc;
     // the state is the caller's: its trigOffset (read back, 4 bytes) is the hint when it is in the
     // float increments' domain (an integer in [0, 2^24]); unknown otherwise (every runner launched

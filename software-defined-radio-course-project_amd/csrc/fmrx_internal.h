@@ -132,6 +132,10 @@ struct PllHint {
     bool known = false;
     double trig_lo = 0.0, trig_hi = 0.0;
     StageTimer* timer = nullptr;  // diagnostic stage timing (null: off)
+    // pll_demoted_kernel once after the call's runner launches (a demoted stream's later launches
+    // skip it) instead of after each runner range: the pipelined engine's chunks, where each of its
+    // launches waited ~0.3 ms for CUs the stage kernels beside the chains hold
+    bool demote_once = false;
 };
 // nco = false: the NCO pass is left to the caller (launch_pll_nco with the same io, n, stride,
 // side and st, on any stream ordered after this launch and before `side` is reused).

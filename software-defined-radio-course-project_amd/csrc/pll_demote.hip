@@ -39,7 +39,7 @@ constexpr int kDemNB = kPllBatch;       // steps a batch (verified as one)
 constexpr int kDemSB = 16;              // batches a sub-segment
 constexpr int kDemL = kDemNB * kDemSB;  // steps a sub-segment
 #ifndef FMRX_DEM_W
-#define FMRX_DEM_W 4
+#define FMRX_DEM_W 2  // (4 until the r06 A/B: the same speed; half the CU to wait for at dispatch)
 #endif
 constexpr int kDemW = FMRX_DEM_W;       // waves: the chain and the checkers
 

@@ -1492,9 +1492,11 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         // the interval's verdict: every trigArg's lane inside its step's candidates, no NaN e
         // taken (the phase), the start state in pll_batch_fast's range; test hooks force misses
         const bool lane_bad = t < NI && (uint32_t)row - off >= (uint32_t)NC;
-        const bool bad = __builtin_amdgcn_ballot_w64(lane_bad) != 0 || !(phase == phase) ||
-                         !(fabsf(phase0) < kPllMaxPhase && fabsf(integ0) < kPllMaxInteg) || i == min(miss, ni) ||
-                         i == inj;
+        // (one ballot over the lane test and the uniform ones: provably uniform, an SGPR -- the redo
+        // branch scalar and pll_demote's history SALU work, no readfirstlane round trip)
+        const bool bad = __builtin_amdgcn_ballot_w64(lane_bad || !(phase == phase) ||
+                                                     !(fabsf(phase0) < kPllMaxPhase && fabsf(integ0) < kPllMaxInteg)) != 0 ||
+                         i == min(miss, ni) || i == inj;
         if (bad) {  // uniform: redo the interval exactly from its start (the chain stores it)
             n_redo++;
             n_inj += i == inj ? 1 : 0;
@@ -1511,7 +1513,7 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
             carry_exact((float)c.x, i + 1);
         }
         if (t < NI) srow[is][t] = row;
-        prev_bad = (uint32_t)__builtin_amdgcn_readfirstlane(bad ? 1 : 0);  // (scalar: no divergent loop)
+        prev_bad = bad ? 1u : 0u;
         sst[is] = make_float4(integ, phase, __builtin_bit_cast(float, bad ? 1 : 0), __builtin_bit_cast(float, leave ? 1 : 0));
         sexact[is] = bad ? 1 : 0;
         const unsigned long long p1 = PROF_T();
@@ -1869,9 +1871,10 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
         // the interval's verdict: no NaN e taken (the phase) or carried (the last trigArg's), the
         // start state in pll_batch_fast's range; test hooks force misses
         const float ce = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cE), cC));
-        const bool bad = !(phase == phase) || !(ce == ce) ||
-                         !(fabsf(phase0) < kPllMaxPhase && fabsf(integ0) < kPllMaxInteg) || i == min(miss, ni) ||
-                         i == inj;
+        // (one ballot: provably uniform, an SGPR -- the redo branch scalar, pll_demote's history SALU)
+        const bool bad = __builtin_amdgcn_ballot_w64(!(phase == phase) || !(ce == ce) ||
+                                                     !(fabsf(phase0) < kPllMaxPhase && fabsf(integ0) < kPllMaxInteg)) != 0 ||
+                         i == min(miss, ni) || i == inj;
         if (bad) {  // uniform: redo the interval exactly from its start (the chain stores it)
             n_redo++;
             n_inj += i == inj ? 1 : 0;
@@ -1890,7 +1893,7 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
 #pragma unroll
         for (int r = 0; r < NRW; r++)
             if (t + 64 * r < NI) srow[is][t + 64 * r] = row[r];
-        prev_bad = (uint32_t)__builtin_amdgcn_readfirstlane(bad ? 1 : 0);  // (scalar: no divergent loop)
+        prev_bad = bad ? 1u : 0u;
         sst[is] = make_float4(integ, phase, __builtin_bit_cast(float, bad ? 1 : 0), __builtin_bit_cast(float, leave ? 1 : 0));
         sexact[is] = bad ? 1 : 0;
         const unsigned long long p1 = PROF_T();

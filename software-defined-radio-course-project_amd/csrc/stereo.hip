@@ -1129,9 +1129,10 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     // form's first interval (the count forms) and its steps past the last whole interval (all
     // forms) run on the exact path at ~400 ns a step -- up to 255 steps a call, every call
     const bool short_call = (size_t)n < kPllShortCall;
-    // pll_demoted_kernel, ONCE a call after its runner launches (a demoted stream's later launches
-    // only add their steps to its hand-off): each launch of it waits for whole CUs (448 VGPRs a
-    // wave), so one per runner range stalled configs[4]'s pipeline ~11 ms (profiles/r06/demote_probe/)
+    // pll_demoted_kernel after each runner range that may demote, or with hint.demote_once ONCE a
+    // call after its runner launches (a demoted stream's later launches only add their steps to its
+    // hand-off): beside the pipelined engine's stage kernels each launch of it waited for CUs, ~11 ms
+    // of configs[4] at one a range (profiles/r06/demote_probe/)
     size_t dem_from = (size_t)n;
     auto run = [&](int form, bool cnt, size_t j, size_t e) {
         const int kind = cnt ? kStCnt17 + (form - 17)
@@ -1148,9 +1149,17 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
                 launch_pll_pipe(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j, (size_t)n,
                                 inject, pipe_miss, form, spec_stats, hint.redos);
             // a launch that may demote a stream (kPllDemoteMinIntervals, the runner's own rule): the
-            // demoted kernel follows the call's last runner launch, from the first such launch on
-            if ((e - j) >= (size_t)kPllDemoteMinIntervals * (size_t)pll_form_interval(form, cnt))
-                dem_from = std::min(dem_from, j);
+            // demoted kernel runs the rest of its range right after it, or (demote_once) follows the
+            // call's last runner launch, from the first such launch on
+            if ((e - j) >= (size_t)kPllDemoteMinIntervals * (size_t)pll_form_interval(form, cnt)) {
+                if (hint.demote_once)
+                    dem_from = std::min(dem_from, j);
+#ifndef FMRX_AB_NO_DEMOTED_LAUNCH
+                else
+                    idx_rc |= launch_pll_demoted(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st,
+                                                 args + j, (size_t)n, inject, spec_stats);
+#endif
+            }
         });
     };
     for (size_t j = n_seg; pipe && j < (size_t)n;) {

@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=60.0)
     ap.add_argument("--repeats", type=int, default=3)
+    ap.add_argument("--profile", action="store_true", help="one more call with the stage timer: ns a step per regime")
     args = ap.parse_args()
     import torch
 
@@ -27,13 +28,21 @@ def main():
     fm = iqgen.load_fmrx()
     dmod = iqgen.load_module("dist")
     nb = int(args.seconds * 2400000 * 2 // 12800)
+    prof = None
+    if args.profile:
+        sys.path.insert(0, REPO)
+        import bench
+        prof = bench.stage_latency
     res = dmod.streams_leg(fm, 256, args.seconds, 1, 0, 0, expect=iqgen.stream_hashes(256, nb) or None,
-                           repeats=args.repeats)
+                           repeats=args.repeats, profile=prof)
     r = res.get("redos", {})
+    lat = res.get("latency") or {}
     print(json.dumps({"lib": fm.LIB_PATH, "median": res.get("median"), "runs": res.get("runs"),
                       "bit_exact": res.get("bit_exact_vs_reference"), "demoted_streams": r.get("demoted_streams"),
                       "demoted_steps_per_range": r.get("demoted_steps_per_range"),
-                      "redos_total_per_range": r.get("total_per_range")}), flush=True)
+                      "redos_total_per_range": r.get("total_per_range"),
+                      "regimes_ns": {k: v["ns_per_step"] for k, v in (lat.get("regimes") or {}).items()},
+                      "stage_ms": lat.get("stage_ms")}), flush=True)
 
 
 if __name__ == "__main__":
