@@ -35,6 +35,14 @@
 namespace fmrx {
 namespace {
 
+// the helpers inlined (466 VGPRs, the runners' 16 B of scratch; unlocked streams 70-78 ns a step
+// against 76-78 out of line, profiles/r06/demote_probe/r06v_*) -- or, A/B build FMRX_AB_DEM_NOINLINE,
+// out of line (their frames on the stack: 528 B of scratch a lane)
+#ifdef FMRX_AB_DEM_NOINLINE
+#define FMRX_DEM_FN __device__ __noinline__
+#else
+#define FMRX_DEM_FN __device__ __attribute__((always_inline))
+#endif
 constexpr int kDemNB = kPllBatch;       // steps a batch (verified as one)
 constexpr int kDemSB = 16;              // batches a sub-segment
 constexpr int kDemL = kDemNB * kDemSB;  // steps a sub-segment
@@ -54,7 +62,7 @@ __device__ inline double dem_iv(float v) {  // pll_check_kernel's 1/v (pll_side'
 // batch that does not certify redone with pll_step (pll_redo) from its start.  Every lane of the
 // wave runs this stream (the chain), lane parity picking sin or cos.  Outside the trigOffset domain
 // pll_side assumes (integer-valued, <= 2^24): pll_redo throughout.
-__device__ __noinline__ PllPair pll_run_fast(PllState p, PllCtx ctx, const float* xb, float* ob, int n, float Ki,
+FMRX_DEM_FN PllPair pll_run_fast(PllState p, PllCtx ctx, const float* xb, float* ob, int n, float Ki,
                                              float Kp, double step) {
     constexpr int NB = kDemNB;
     const SplitCoef sc = split_coef((threadIdx.x & 1) != 0);
@@ -93,7 +101,7 @@ __device__ __noinline__ PllPair pll_run_fast(PllState p, PllCtx ctx, const float
 
 // the state before step k of the range from (integ, phase) after step k - 1 and that step's
 // trigArg a (pll_state_at: fbI, fbQ and the context from the exact sin/cos of a)
-__device__ __noinline__ PllPair dem_state(float integ, float phase, float t0, int k, float a) {
+FMRX_DEM_FN PllPair dem_state(float integ, float phase, float t0, int k, float a) {
     PllPair r;
     r.ctx = PllCtx{};
     pll_state_at(r.p, r.ctx, integ, phase, t0, (long long)k, a, DeviceLib{});
@@ -102,7 +110,7 @@ __device__ __noinline__ PllPair dem_state(float integ, float phase, float t0, in
 
 // One checker lane: batch b of a sub-segment whose first step is J0, from (integ, phase, a) before
 // it; tg: the chain's trigArgs of the batch, (ei, ep) its end state.  True when they are exact.
-__device__ __noinline__ bool dem_verify(const float* x, int J, float integ, float phase, float a, float t0, double step,
+FMRX_DEM_FN bool dem_verify(const float* x, int J, float integ, float phase, float a, float t0, double step,
                                        float Ki, float Kp, const float* tg, float ei, float ep) {
     constexpr int NB = kDemNB;
     PllPair z = dem_state(integ, phase, t0, J, a);

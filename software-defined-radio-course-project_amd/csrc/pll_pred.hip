@@ -1380,24 +1380,21 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         __syncthreads();  // (prologue)
         unsigned long long ev_body = 0, ev_wait = 0;
         // pll_demote is the chain's (its verdicts are at hand there, a few scalar ops an interval):
-        // when it leaves after interval i - 1 it says so in that interval's state word (w), and the
-        // evaluators store that interval's trigArgs and leave too, without another barrier
+        // it may leave only after the last interval of one of these groups of RD, saying so in
+        // that interval's state word (w); the evaluators look once a group, store that interval's
+        // trigArgs and leave too, without another barrier (a test per interval cost the index forms
+        // ~3 ns a step: the evaluators set their pace)
         bool left = false;
-        for (int i0 = 1; i0 <= ni && !left; i0 += RD) {
+        for (int i0 = 1; i0 <= ni; i0 += RD) {
             unroll_ic(
                 [&](auto uc) {
                     constexpr int u = decltype(uc)::value;
                     constexpr int sl = (2 + u) % RD;  // slot of interval i + 1
                     const int i = i0 + u;
-                    if (i <= ni && !left) {
+                    if (i <= ni) {
                         const unsigned long long p0 = PROF_T();
-                        // the chain's state at interval i's start (and whether it left there)
+                        // the chain's state at interval i's start
                         const float4 rs = sst[(i - 1) & 3];
-                        if (!kAbNoDemote && __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, rs.w)) != 0) {
-                            store(i - 1);
-                            left = true;
-                            return;
-                        }
                         if (i + 1 <= ni) {
                             put(i + 1, rs.y, vq[sl]);  // from the phase at interval i's start
                             hook_poison(i + 1);
@@ -1411,6 +1408,14 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
                     }
                 },
                 std::make_integer_sequence<int, RD>{});
+            // (at the group's end, not its start: a test skipped on the first group made LLVM peel
+            // a whole group)
+            if (!kAbNoDemote &&
+                __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, sst[(i0 + RD - 1) & 3].w)) != 0) {
+                store(i0 + RD - 1);
+                left = true;
+                break;
+            }
         }
         if (!left) store(ni);
 #ifdef FMRX_AB_PROF
@@ -1450,15 +1455,18 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
     uint32_t hist = 0;
     unsigned long long n_redo = 0, n_inj = 0, ch_body = 0, ch_wait = 0;
     const uint32_t off = (uint32_t)(NC * ((t & (NI - 1)) % SPP));  // lane t's step's lane offset
-    uint32_t prev_bad = 0;  // the last interval's verdict (SGPR)
-    for (int i = 1; i <= ni && dem_i == 0; i++) {
+    // the last interval's verdict (SGPR); the start values are 0 but not constants to the compiler
+    // (constants there made LLVM peel the first interval: a second copy of the chain loop)
+    uint32_t prev_bad = n < 0 ? 1u : 0u;
+    hist = n < 0 ? 1u : 0u;
+    for (int i = 1; i <= ni; i++) {
         const unsigned long long p0 = PROF_T();
         const int is = i & 3;
         const float integ0 = integ, phase0 = phase;
         // the verdicts up to interval i - 1 decide whether the chain leaves after this one: scalar
         // work at the interval's start, off the chain's path (at its end it delayed the barrier)
         hist = (hist << 1) | prev_bad;
-        const bool leave = !kAbNoDemote && i < ni && n >= kPllDemoteMinIntervals * NI &&
+        const bool leave = !kAbNoDemote && i % RD == 0 && i < ni && n >= kPllDemoteMinIntervals * NI &&
                            __builtin_popcount(hist) >= kPllDemoteMissesIdx;
         // the interval's data before its steps (NI 16-byte broadcasts, NR row reads)
         float4 D[NI];
@@ -1520,7 +1528,10 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         __syncthreads();
         ch_body += p1 - p0;
         ch_wait += PROF_T() - p1;
-        if (leave) dem_i = i;  // (the evaluators leave after this interval's barrier too)
+        if (leave) {  // (the evaluators leave after this interval's barrier too)
+            dem_i = i;
+            break;
+        }
     }
 #ifdef FMRX_AB_PROF
     if (t == 0) {
@@ -1754,24 +1765,21 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
         __syncthreads();  // (prologue)
         unsigned long long ev_body = 0, ev_wait = 0;
         // pll_demote is the chain's (its verdicts are at hand there, a few scalar ops an interval):
-        // when it leaves after interval i - 1 it says so in that interval's state word (w), and the
-        // evaluators store that interval's trigArgs and leave too, without another barrier
+        // it may leave only after the last interval of one of these groups of RD, saying so in
+        // that interval's state word (w); the evaluators look once a group, store that interval's
+        // trigArgs and leave too, without another barrier (a test per interval cost the index forms
+        // ~3 ns a step: the evaluators set their pace)
         bool left = false;
-        for (int i0 = 1; i0 <= ni && !left; i0 += RD) {
+        for (int i0 = 1; i0 <= ni; i0 += RD) {
             unroll_ic(
                 [&](auto uc) {
                     constexpr int u = decltype(uc)::value;
                     constexpr int sl = (2 + u) % RD;  // slot of interval i + 1
                     const int i = i0 + u;
-                    if (i <= ni && !left) {
+                    if (i <= ni) {
                         const unsigned long long p0 = PROF_T();
-                        // the chain's state at interval i's start (and whether it left there)
+                        // the chain's state at interval i's start
                         const float4 rs = sst[(i - 1) & 3];
-                        if (!kAbNoDemote && __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, rs.w)) != 0) {
-                            store(i - 1);
-                            left = true;
-                            return;
-                        }
                         if (i + 1 <= ni) {
                             put(i + 1, rs.y, vq[sl]);  // from the phase at interval i's start
                             hook_poison(i + 1);
@@ -1785,6 +1793,14 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
                     }
                 },
                 std::make_integer_sequence<int, RD>{});
+            // (at the group's end, not its start: a test skipped on the first group made LLVM peel
+            // a whole group)
+            if (!kAbNoDemote &&
+                __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, sst[(i0 + RD - 1) & 3].w)) != 0) {
+                store(i0 + RD - 1);
+                left = true;
+                break;
+            }
         }
         if (!left) store(ni);
 #ifdef FMRX_AB_PROF
@@ -1824,7 +1840,10 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
     uint32_t hist = 0;
     unsigned long long n_redo = 0, n_inj = 0, ch_body = 0, ch_wait = 0;
     const int ls = t < NP ? t : NP - 1;  // this lane's row slot (lanes past the row read its last)
-    uint32_t prev_bad = 0;  // the last interval's verdict (SGPR)
+    // the last interval's verdict (SGPR); the start values are 0 but not constants to the compiler
+    // (constants there made LLVM peel the first interval: a second copy of the chain loop)
+    uint32_t prev_bad = n < 0 ? 1u : 0u;
+    hist = n < 0 ? 1u : 0u;
     for (int i = 1; i <= ni && dem_i == 0; i++) {
         const unsigned long long p0 = PROF_T();
         const int is = i & 3;
@@ -1832,7 +1851,7 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
         // the verdicts up to interval i - 1 decide whether the chain leaves after this one: scalar
         // work at the interval's start, off the chain's path (at its end it delayed the barrier)
         hist = (hist << 1) | prev_bad;
-        const bool leave = !kAbNoDemote && i < ni && n >= kPllDemoteMinIntervals * NI &&
+        const bool leave = !kAbNoDemote && i % RD == 0 && i < ni && n >= kPllDemoteMinIntervals * NI &&
                            __builtin_popcount(hist) >= kPllDemoteMisses;
         int row[NRW] = {};
         unroll_ic(
