@@ -196,10 +196,11 @@ int launch_pll_cnt(hipStream_t s, const float* io, int n, int n_streams, size_t 
 // steps an interval of launch_pll's form (17-23) on the count runner (cnt) or the index / three-wave
 // runner: a range of fewer than 24 intervals cannot demote (launch_pll skips pll_demoted_kernel)
 int pll_form_interval(int form, bool cnt);
-// launch_pll: a call of fewer steps a stream than kPllShortCall runs only 16-step forms; a range of
-// fewer than kPllShortIntervals long intervals too; a long form's tail past its last whole interval
-// of at least kPllShortTail steps runs on the 16-step form (three 16-step intervals)
-constexpr size_t kPllShortCall = 4096, kPllShortIntervals = 4, kPllShortTail = 48;
+// launch_pll: a range of fewer than kPllShortIntervals of its form's long intervals runs on the
+// 16-step forms (in a call of fewer than kPllShortCall steps a stream, to the call's end); a long
+// form's tail past its last whole interval of at least kPllShortTail steps runs on the 16-step form
+// (three 16-step intervals; a long launch needs two whole intervals or it runs exactly)
+constexpr size_t kPllShortCall = 4096, kPllShortIntervals = 2, kPllShortTail = 48;
 int launch_pll_demoted(hipStream_t s, const float* io, int n, int n_streams, size_t stride, double step,
                        float norm_bw, float* st, float* out, size_t ostride, int inject, unsigned long long* stats);
 // fmrx_debug_pll_redos: per stream kPllRedoSlots u32, by the trigOffset range r of the runner's

@@ -1125,9 +1125,12 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     // 16-step five-candidate form, [2^21, 2^22) the 64-step one, from 2^22 (the stick included)
     // three candidates
     int idx_rc = 0;
-    // a short call (the per-block seam: 640 steps a call) runs the 16-step forms only: a long
-    // form's first interval (the count forms) and its steps past the last whole interval (all
-    // forms) run on the exact path at ~400 ns a step -- up to 255 steps a call, every call
+    // A range of fewer than kPllShortIntervals of its form's long intervals runs on the 16-step
+    // forms (the index runner below 2^20, the wide three-wave form 24 from 2^20: in a short call to
+    // the call's end); a long form's steps past its last whole interval go to the 16-step form too
+    // (on the exact path they cost ~400 ns a step).  The first interval of every form is predicted,
+    // so a long form pays nothing extra for a short call: the per-block seam's 640 steps are 10
+    // count-form intervals in [2^19, 2^20), 5 in [2^20, 2^22), 2 + a 128-step tail past 2^22.
     const bool short_call = (size_t)n < kPllShortCall;
     // pll_demoted_kernel after each runner range that may demote, or with hint.demote_once ONCE a
     // call after its runner launches (a demoted stream's later launches only add their steps to its
@@ -1177,7 +1180,7 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         const size_t len = e - j, ni = (size_t)pll_form_interval(form, cnt);
         // the 16-step forms (the index runner below 2^20, the wide three-wave form 24 from 2^20 to the
         // end of a short call) for a short call and for a range of few long intervals
-        if (ni > 16 && (short_call || len < kPllShortIntervals * ni)) {
+        if (ni > 16 && len < kPllShortIntervals * ni) {
             if (form >= 20 && short_call) e = (size_t)n;
             run(form >= 20 ? 24 : form, false, j, e);
             j = e;
