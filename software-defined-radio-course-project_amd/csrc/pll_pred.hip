@@ -2039,7 +2039,10 @@ void launch_pll_pipe(hipStream_t s, const float* io, int n, int n_streams, size_
     reg_pred_prof();
 #endif
     if (n <= 0) return;
-    if (form == 24)  // the short-call form: any trigOffset from 2^20, 16-step intervals
+    if (form == 25)  // short calls from 2^22: three candidates in 128-step intervals (640 = 5 of them)
+        hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 8, FMRX_PIPE_RD, 3>), dim3(n_streams), dim3(192), 0, s, io, n,
+                           n_streams, stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
+    else if (form == 24)  // the short-call form: any trigOffset from 2^20, 16-step intervals
         hipLaunchKernelGGL((pll_pipe_kernel<kPllBatch, 1, FMRX_PIPE_RD, 5, false, true>), dim3(n_streams), dim3(192), 0, s,
                            io, n, n_streams, stride, step, norm_bw, st, out, ostride, inject, miss, stats, redos);
     else if (form == 23)
@@ -2139,6 +2142,7 @@ static int cnt_launch(hipStream_t s, const float* io, int n, int n_streams, size
 int pll_form_interval(int form, bool cnt) {
     if (cnt) return form <= 18 ? FMRX_CNT17_NI : form == 19 ? FMRX_CNT19_NI : form == 20 ? FMRX_CNT20_NI : 64;
     if (form < 20) return 16;  // the index runner
+    if (form == 25) return kPllBatch * 8;
     return form == 20 || form == 24 ? kPllBatch : form == 21 ? kPllBatch * FMRX_PIPE21_BPI
          : form == 22 ? kPllBatch * FMRX_PIPE22_BPI : kPllBatch * FMRX_STICK_BPI;
 }

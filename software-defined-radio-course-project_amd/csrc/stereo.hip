@@ -1140,7 +1140,8 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
     auto run = [&](int form, bool cnt, size_t j, size_t e) {
         const int kind = cnt ? kStCnt17 + (form - 17)
                        : form == 17 ? kStIdx17 : form == 18 ? kStIdx18 : form == 19 ? kStIdx19
-                       : form == 20 || form == 24 ? kStPipe20 : form == 21 ? kStPipe21 : form == 22 ? kStPipe22 : kStStick;
+                       : form == 20 || form == 24 ? kStPipe20 : form == 21 ? kStPipe21 : form == 22 || form == 25 ? kStPipe22
+                       : kStStick;
         timed(kind, (double)(e - j), [&] {
             if (cnt)
                 idx_rc |= launch_pll_cnt(s, io + j, (int)(e - j), n_streams, stride, step, norm_bw, st, args + j,
@@ -1169,7 +1170,7 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
         const double t = std::min(hlo + (double)j, (double)kPllTrigStick);
         // form 23 (the stuck trigOffset, 2^24): the three-candidate runner's stick form (pll_stick)
         const bool stick = kn.stick != 0;
-        const int form = t < 262144.0 ? 17 : t < 524288.0 ? 18 : t < (double)kPllPipeMinLow ? 19
+        int form = t < 262144.0 ? 17 : t < 524288.0 ? 18 : t < (double)kPllPipeMinLow ? 19
                        : t < (double)kPllPipeMin5 ? 20 : t < (double)kPllPipeMin ? 21
                        : (!stick || t < (double)kPllTrigStick) ? 22 : 23;
         const double edge = form == 17 ? 262144.0 : form == 18 ? 524288.0 : form == 19 ? (double)kPllPipeMinLow
@@ -1177,6 +1178,12 @@ int launch_pll(float* io, int n, int n_streams, size_t stride, float freq, float
                           : form == 22 && stick ? (double)kPllTrigStick : 0.0;
         size_t e = edge == 0.0 ? (size_t)n : std::min((size_t)(edge - hlo), (size_t)n);
         const bool cnt = form < 22 && ((kn.cnt >> (form - 17)) & 1) && kPllIdxSimds * n_streams <= n_simd;
+        // a short call from 2^22 on the three-candidate form in 128-step intervals (launch form 25):
+        // the per-block seam's 640 steps are 5 of them, of 256-step ones 2 and a tail
+        if (short_call && form >= 22) {
+            form = 25;
+            e = (size_t)n;
+        }
         const size_t len = e - j, ni = (size_t)pll_form_interval(form, cnt);
         // the 16-step forms (the index runner below 2^20, the wide three-wave form 24 from 2^20 to the
         // end of a short call) for a short call and for a range of few long intervals
