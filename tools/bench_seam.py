@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=3000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--cli-mib", type=int, default=256)
+    ap.add_argument("--queue", type=int, default=3, help="the two-thread leg's queue depth (project.cpp QUEUE_CAPACITY)")
+    ap.add_argument("--legs", default="serial,two_threads,native,cli", help="comma-separated legs to run")
     args = ap.parse_args()
     import iqgen
 
@@ -85,7 +87,7 @@ def main():
     pcm2 = np.zeros_like(pcm)
     pcm2_p = pcm2.ctypes.data
     with fm.Receiver(0, fm.STEREO) as rx_rf, fm.Receiver(0, fm.STEREO) as rx_au:
-        q = queue.Queue(maxsize=16)  # project.cpp QUEUE_CAPACITY-like bound
+        q = queue.Queue(maxsize=args.queue)  # project.cpp:17 QUEUE_CAPACITY (3; the deepest measured best)
         err = []
         t_start = [0.0]
 
@@ -118,12 +120,17 @@ def main():
 
     # the same two legs from C++ (bin/fmrx_seam: project.cpp's own call pattern, no interpreter
     # between the calls), on the same stream
+    legs = set(args.legs.split(","))
     seam_exe = os.path.join(os.path.dirname(fm.LIB_PATH), "bin", "fmrx_seam")
-    r = subprocess.run([seam_exe, "--blocks", str(args.blocks), "--warmup", str(args.warmup)],
+    r = None if "native" not in legs else subprocess.run([seam_exe, "--blocks", str(args.blocks), "--warmup", str(args.warmup)],
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=600)
-    if r.returncode != 0:
-        raise SystemExit(f"{seam_exe} failed ({r.returncode}): {r.stderr.decode()[-400:]}")
-    res["native"] = json.loads(r.stdout.decode())
+    if r is not None:
+        if r.returncode != 0:
+            raise SystemExit(f"{seam_exe} failed ({r.returncode}): {r.stderr.decode()[-400:]}")
+        res["native"] = json.loads(r.stdout.decode())
+    if "cli" not in legs:
+        print(json.dumps(res), flush=True)
+        return
 
     # the CLI on the same synthetic stream from a file, default batch and the large batch
     exe = os.path.join(os.path.dirname(fm.LIB_PATH), "bin", "fmrx")
