@@ -662,6 +662,25 @@ def test_seam_calls_in_every_pll_regime(fmrx):
     assert sha(np.concatenate(parts)) == h["pcm_sha256"]
 
 
+def test_seam_driver_native(fmrx):
+    """bin/fmrx_seam (csrc/seam_bench.cpp): the per-block seam from C++ in project.cpp's call
+    pattern, serially on one context and on two threads / two contexts with a depth-3 queue, from
+    block 0 and from past the 2^22 trigOffset: the two legs' PCM are equal (exit 0) and the JSON
+    line is well formed."""
+    import json
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(fmrx.LIB_PATH), "bin", "fmrx_seam")
+    for start in (0, 6600):
+        r = subprocess.run([exe, "--blocks", "300", "--warmup", "10", "--start", str(start)], capture_output=True,
+                           timeout=240)
+        assert r.returncode == 0, r.stderr.decode()[-400:]
+        d = json.loads(r.stdout.decode())
+        assert d["two_threads"]["pcm_equals_serial"] and d["start_block"] == start
+        assert d["serial"]["x_realtime"] > 0 and d["two_threads"]["x_realtime"] > 0
+
+
 def test_stereo_long_hash_three_streams(fmrx):
     """The saturated-segment runner (pll_sat.hip) with several waves: three copies of the 72 s
     long run in one 3-stream call, each stream's PCM against the reference build's hash."""

@@ -28,6 +28,18 @@ def test_library_exports_every_header_symbol(fmrx):
     assert set(fmrx.PROTOTYPES) == set(syms), "Python prototypes out of sync with include/fmrx.h"
 
 
+def test_seam_driver_built(fmrx):
+    """bin/fmrx_seam (the per-block seam from C++, tools/bench_seam.py's native legs) is built beside
+    the library and resolves it (ldd: no missing libraries)."""
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(fmrx.LIB_PATH), "bin", "fmrx_seam")
+    assert os.access(exe, os.X_OK), exe
+    r = subprocess.run(["ldd", exe], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 0 and "not found" not in r.stdout and "libfmrx.so" in r.stdout, r.stdout
+
+
 def test_version_string(fmrx):
     assert b"gfx950" in fmrx.lib().fmrx_version()
 
