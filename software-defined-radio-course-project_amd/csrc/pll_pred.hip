@@ -1135,7 +1135,8 @@ __global__ void __launch_bounds__(192) __attribute__((amdgpu_waves_per_eu(1, 1))
             }
             integ = q.integ;
             phase = q.phase;
-            if (over && n >= kPllDemoteMinIntervals * NI) {  // demoted: the evaluators leave after B1.5,
+            if (over && n >= kPllDemoteMinIntervals * NI &&  // demoted: the evaluators leave after B1.5,
+                __builtin_amdgcn_ballot_w64(fabsf(q.phase) < kPllMaxPhase && fabsf(q.integ) < kPllMaxInteg) != 0) {
                                                                // pll_demoted_kernel runs the rest
                 sdemote = 1;
                 __syncthreads();  // B1.5
@@ -1466,7 +1467,10 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         // the verdicts up to interval i - 1 decide whether the chain leaves after this one: scalar
         // work at the interval's start, off the chain's path (at its end it delayed the barrier)
         hist = (hist << 1) | prev_bad;
+        // (and only from a state the demoted kernel's fast batches take: beyond their range every
+        // interval misses for that reason alone, and the exact path is what runs either way)
         const bool leave = !kAbNoDemote && i % RD == 0 && i < ni && n >= kPllDemoteMinIntervals * NI &&
+                           __builtin_amdgcn_ballot_w64(fabsf(phase) < kPllMaxPhase && fabsf(integ) < kPllMaxInteg) != 0 &&
                            __builtin_popcount(hist) >= kPllDemoteMissesIdx;
         // the interval's data before its steps (NI 16-byte broadcasts, NR row reads)
         float4 D[NI];
@@ -1851,7 +1855,10 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
         // the verdicts up to interval i - 1 decide whether the chain leaves after this one: scalar
         // work at the interval's start, off the chain's path (at its end it delayed the barrier)
         hist = (hist << 1) | prev_bad;
+        // (and only from a state the demoted kernel's fast batches take: beyond their range every
+        // interval misses for that reason alone, and the exact path is what runs either way)
         const bool leave = !kAbNoDemote && i % RD == 0 && i < ni && n >= kPllDemoteMinIntervals * NI &&
+                           __builtin_amdgcn_ballot_w64(fabsf(phase) < kPllMaxPhase && fabsf(integ) < kPllMaxInteg) != 0 &&
                            __builtin_popcount(hist) >= kPllDemoteMisses;
         int row[NRW] = {};
         unroll_ic(

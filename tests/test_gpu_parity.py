@@ -860,6 +860,8 @@ def test_primitives(fmrx, taps_golden):
     (0.5, 0.0, 19000, 240000, 300, 0),               # non-integer trigOffset: exact path only
     (3.0e7, 0.0, 19000, 240000, 300, 0),             # past 2^24: exact path only
     (0.0, 6.0e8, 19000, 240000, 300, 0),             # |phaseEst| beyond the batch's range check
+    (131072.0, 6.0e8, 19000, 240000, 20000, 0),      # the same in the index runner's range: every
+                                                     # interval redone, then the stream demoted
     (0.0, 0.0, 114000, 240000, 2000, 0),             # RDS's 114 kHz loop
     (0.0, 0.0, 19000, 35280000, 2000, 0),            # mode 2's upsampled fs (project.cpp:166)
     (0.0, 0.0, 19000, 240000, 1000, 1),              # unaligned samples: exact path only
