@@ -1468,10 +1468,12 @@ pll_idx_kernel(const float* io, int n, int n_streams, size_t stride, double step
         // work at the interval's start, off the chain's path (at its end it delayed the barrier)
         hist = (hist << 1) | prev_bad;
         // (and only from a state the demoted kernel's fast batches take: beyond their range every
-        // interval misses for that reason alone, and the exact path is what runs either way)
-        const bool leave = !kAbNoDemote && i % RD == 0 && i < ni && n >= kPllDemoteMinIntervals * NI &&
-                           __builtin_amdgcn_ballot_w64(fabsf(phase) < kPllMaxPhase && fabsf(integ) < kPllMaxInteg) != 0 &&
-                           __builtin_popcount(hist) >= kPllDemoteMissesIdx;
+        // interval misses for that reason alone, and the exact path is what runs either way; the
+        // range test only then, the common path SALU work only)
+        bool leave = false;
+        if (!kAbNoDemote && i % RD == 0 && i < ni && n >= kPllDemoteMinIntervals * NI &&
+            __builtin_popcount(hist) >= kPllDemoteMissesIdx)  // (scalar, nearly always false: a branch
+            leave = __builtin_amdgcn_ballot_w64(fabsf(phase) < kPllMaxPhase && fabsf(integ) < kPllMaxInteg) != 0;
         // the interval's data before its steps (NI 16-byte broadcasts, NR row reads)
         float4 D[NI];
         float E[NR];
@@ -1856,10 +1858,12 @@ pll_cnt_kernel(const float* io, int n, int n_streams, size_t stride, double step
         // work at the interval's start, off the chain's path (at its end it delayed the barrier)
         hist = (hist << 1) | prev_bad;
         // (and only from a state the demoted kernel's fast batches take: beyond their range every
-        // interval misses for that reason alone, and the exact path is what runs either way)
-        const bool leave = !kAbNoDemote && i % RD == 0 && i < ni && n >= kPllDemoteMinIntervals * NI &&
-                           __builtin_amdgcn_ballot_w64(fabsf(phase) < kPllMaxPhase && fabsf(integ) < kPllMaxInteg) != 0 &&
-                           __builtin_popcount(hist) >= kPllDemoteMisses;
+        // interval misses for that reason alone, and the exact path is what runs either way; the
+        // range test only then, the common path SALU work only)
+        bool leave = false;
+        if (!kAbNoDemote && i % RD == 0 && i < ni && n >= kPllDemoteMinIntervals * NI &&
+            __builtin_popcount(hist) >= kPllDemoteMisses)  // (scalar, nearly always false: a branch
+            leave = __builtin_amdgcn_ballot_w64(fabsf(phase) < kPllMaxPhase && fabsf(integ) < kPllMaxInteg) != 0;
         int row[NRW] = {};
         unroll_ic(
             [&](auto hc) {
